@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident chunk reduce on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Step = one pass of the hot path over one batch of synthetic input: one
+pgk_reduce (include/pgk.h -- the kernel that replaces the reference's
+reduce_inplace, src/pg.c:151-159) of a device-resident chunk, BASELINE config 2:
+DT_DOUBLE OP_SUM over 256 MiB (dst op= src).  Inputs are resident in HBM
+before the timed region; 4 dst/src pairs (2 GiB) rotate so the 256 MiB
+Infinity Cache cannot serve them.
+
+At N > 1 every rank (one process per GPU) runs the same per-GPU workload
+concurrently: weak scaling, no collective in the data path of the measured
+step.  The ring itself (RCCL over xGMI + the same kernel, through the public
+pg_reduce_scatter) is timed after the main measurement and reported in the
+same JSON line under "ring" (BASELINE configs 3/4 shapes).
+
+value      = whole-job GiB/s of algorithmic HBM traffic, 3 * n * 8 bytes per
+             step (read dst, read src, write dst), summed over ranks, divided by
+             the max-over-ranks wall time of the K timed steps.
+roofline   = the kernel's achieved GB/s (same bytes / mean per-launch HIP-event
+             duration on the launch stream) against 8000 GB/s HBM3E peak.
+cpu_baseline = the reference's own reduce loop (oracle/_ref, compiled from the
+             reference src/pg.c) or its C restatement, 1 pinned host core,
+             rank 0 at N = 1 only, on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import pgamd  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_ELEMS = 1 << 25                # 256 MiB of float64 (BASELINE config 2)
+N_PAIRS = 4                      # 4 x (dst, src) = 2 GiB > 256 MiB MALL
+DT, OP = pgamd.DT_DOUBLE, pgamd.OP_SUM
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
+    ap.add_argument("--ring-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def kernel_leg(lib, args, rank, world):
+    """The timed steps.  Returns wall seconds, per-launch ms list."""
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    dst = [torch.rand(N_ELEMS, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(N_PAIRS)]
+    src = [torch.rand(N_ELEMS, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(N_PAIRS)]
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step(i):
+        rc = lib.pgk_reduce(dst[i % N_PAIRS].data_ptr(), src[i % N_PAIRS].data_ptr(), N_ELEMS, DT, OP, sh)
+        if rc != 0:
+            raise RuntimeError(pgamd.last_error())
+
+    for i in range(args.warmup):
+        step(i)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    per_launch_ms = [a.elapsed_time(b) for a, b in ev]
+    del dst, src
+    torch.cuda.empty_cache()
+    return t1 - t0, per_launch_ms
+
+
+def cpu_baseline(args):
+    """Reference reduce loop on 1 pinned host core, bounded sample of the workload."""
+    from oracle.pyoracle import REF_LIB, Oracle, Reference
+    try:
+        impl, kind = Reference(), "reference"
+    except RuntimeError:
+        impl, kind = Oracle(), "port"
+    orc = Oracle()
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except (AttributeError, OSError):
+        pass
+    n = N_ELEMS                                   # the same 256 MiB chunk
+    d = orc.fill(n, DT, OP, 0x5EEDC0DE ^ (2 << 32))
+    s = orc.fill(n, DT, OP, 0x5EEDC0DE ^ (2 << 32) ^ 1)
+    impl.time_reduce(d, s, DT, OP, 1)             # touch pages
+    reps, secs = 0, 0.0
+    while secs < args.cpu_seconds:
+        secs += impl.time_reduce(d, s, DT, OP, 1)
+        reps += 1
+    gibs = 3 * n * 8 * reps / secs / GIB
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(gibs, 3), "unit": "GiB/s (3*n*8 B traffic)", "cores": 1, "kind": kind,
+            "payload_gibs": round(n * 8 * reps / secs / GIB, 3),
+            "sample": f"{reps} x reduce_inplace(double, sum) over 256 MiB chunks, {secs:.1f} s, "
+                      f"1 pinned core of {os.cpu_count()} ({cpu}); "
+                      f"{'oracle/_ref = reference src/pg.c:151-159 compiled -O2' if kind == 'reference' else 'oracle/pg_oracle.c restatement -O2'}"}
+
+
+def load_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (see
+    profiles/README.md): (FETCH_SIZE*2 + WRITE_SIZE) KiB per dispatch, gfx950
+    FETCH_SIZE correction applied by tools/pmc_traffic.py."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    try:
+        d = json.loads(p.read_text())
+        return d.get("reduce_f64_sum_256MiB", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def ring_leg(lib, args, rank, world):
+    """pg_reduce_scatter over RCCL/xGMI, device-resident, BASELINE configs 3/4."""
+    if world == 4:
+        dt, count, cfg = pgamd.DT_INT32, 1 << 28, "config3: 4-GPU ring, int32 sum, 1 GiB/rank"
+    elif world == 8:
+        dt, count, cfg = pgamd.DT_DOUBLE, 1 << 29, "config4: 8-GPU ring, double sum, 4 GiB/rank"
+    else:
+        dt, count, cfg = pgamd.DT_DOUBLE, 1 << 27, f"{world}-GPU ring, double sum, 1 GiB/rank"
+    es = pgamd.ELEM_SIZE[dt]
+    hosts = " ".join(["127.0.0.1"] * world).encode()
+    os.environ["PG_RANK"] = str(rank)
+    os.environ.setdefault("PG_PORT", str(int(os.environ.get("MASTER_PORT", "29500")) + 17))
+    h = ctypes.c_void_p()
+    if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
+        raise RuntimeError("connect_process_group: " + pgamd.last_error())
+    try:
+        tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
+        idx = torch.arange(count, device="cuda", dtype=torch.int64) % 1000
+        x = (idx + rank).to(tdt)
+        off, ln = pgamd.block_range(count, world, rank)
+        out = torch.empty(ln, dtype=tdt, device="cuda")
+        torch.cuda.synchronize()
+        # correctness probe: block r of sum_q (i % 1000 + q) = W*(i % 1000) + W(W-1)/2
+        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h), "ring RS")
+        want = (idx[off:off + ln] * world + world * (world - 1) // 2).to(tdt)
+        ok = bool(torch.equal(out, want))
+        del want, idx
+        barrier(world)
+        t0 = time.perf_counter()
+        ring_us = []
+        for _ in range(args.ring_steps):
+            pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h), "ring RS")
+            ring_us.append(pgamd.stats(h)["ring_us"])
+        barrier(world)
+        wall = max_over_ranks(time.perf_counter() - t0, world) / args.ring_steps
+        hd = pgamd.head(h)
+        ok_all = sum_over_ranks(1.0 if ok else 0.0, world) == world
+        payload = count * es                       # per rank
+        return {"workload": cfg, "ok": ok_all, "ms_per_reduce_scatter": round(wall * 1e3, 3),
+                "algbw_gibs": round(payload / wall / GIB, 2),
+                "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
+                "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
+                "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
+                "transport": "rccl-p2p-xgmi"}
+    finally:
+        lib.pg_close(h)
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup(args)
+    lib = pgamd.load()
+    wall, per_launch_ms = kernel_leg(lib, args, rank, world)
+    wall_max = max_over_ranks(wall, world)
+    bytes_per_step = 3 * N_ELEMS * 8
+    mean_launch_ms = sum_over_ranks(float(np.mean(per_launch_ms)), world) / world
+    achieved_gbs = bytes_per_step / (mean_launch_ms * 1e-3) / 1e9
+    value = world * bytes_per_step * args.steps / wall_max / GIB
+
+    ring = None
+    if world > 1 and not args.no_ring:
+        try:
+            ring = ring_leg(lib, args, rank, world)
+        except Exception as e:  # the primary measurement stands on its own
+            ring = {"error": f"{type(e).__name__}: {e}"}
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        traffic = load_traffic()
+        line = {
+            "metric": "GiB/s device-resident chunk reduce (int32 sum, double sum) at 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (uniform [-1,1) doubles, HBM-resident, 4 rotating 256 MiB dst/src pairs)",
+            "config": {"workload": "BASELINE config 2: pgk_reduce DT_DOUBLE OP_SUM, 256 MiB chunk per GPU "
+                                   "(dst op= src), one reduce per step per GPU",
+                       "chunk_bytes": N_ELEMS * 8, "bytes_per_step_per_gpu": bytes_per_step,
+                       "parallelism": f"replicated per GPU x{world}"},
+            "payload_gibs": round(value / 3, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel_mean_ms": round(mean_launch_ms, 5),
+                         "kernel_min_ms": round(float(np.min(per_launch_ms)), 5)},
+            "cpu_baseline": cpu,
+            "ring": ring,
+            "kernel": pgamd.load().pgk_version().decode(),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

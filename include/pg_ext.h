@@ -1,0 +1,108 @@
+/*
+ * include/pg_ext.h -- extensions of libpg_amd.so beyond the reference surface.
+ *
+ * None of these are needed by a caller of the reference API (include/pg.h).
+ * They expose (a) the ring schedule as data, so the host logic can be tested
+ * without a GPU, (b) transports for single-process operation, and
+ * (c) per-call measurements for the benchmark.
+ */
+#ifndef PG_EXT_H
+#define PG_EXT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* struct pg.transport values.  Selected with PG_TRANSPORT=rccl|loopback. */
+#define PG_TRANSPORT_RCCL     0  /* one process per GPU, RCCL P2P over xGMI (default) */
+#define PG_TRANSPORT_LOOPBACK 1  /* one process, the reference's single-process mock
+                                    schedule (src/pg.c:161-179, :264-321) run on the
+                                    GPU kernel: results equal the reference's own   */
+#define PG_TRANSPORT_THREADS  2  /* W virtual ranks in one process (one thread each)
+                                    sharing one GPU; the hop is a device copy.  Used
+                                    by pgx_sim_run() to exercise the ring executor   */
+#define PG_TRANSPORT_SELF     3  /* world_size == 1 */
+
+/* Ring block partition used by pg_reduce_scatter / pg_all_reduce: block b of
+ * count elements = [b*B, min((b+1)*B, count)) with B = ceil(count/world), the
+ * reference's chunk_offsets() clamping (src/pg.c:126-138).  Elements. */
+int pg_block_range(int count, int world, int block, size_t *off, size_t *len);
+
+/* Buffer roles named by plan steps. */
+#define PG_BUF_NONE   0
+#define PG_BUF_SRC    1   /* this rank's input (count elements)               */
+#define PG_BUF_OUT    2   /* RS: this rank's result block; AG: the full buffer */
+#define PG_BUF_STAGE0 3   /* HBM staging, one block                            */
+#define PG_BUF_STAGE1 4   /* HBM staging, one block                            */
+
+/* One ring step: in one transport group, send `send_bytes` to the right
+ * neighbour and receive `recv_bytes` from the left; then (on the reduce
+ * stream, after the receive) red_dst[i] = red_dst[i] op red_src[i] for
+ * i < red_elems.  Offsets/lengths in bytes except red_elems. */
+struct pg_step {
+  int32_t round;       /* ring round k, 0 .. world-2                          */
+  int32_t batch;       /* steps with equal batch share one transport group    */
+  int32_t seg;         /* segment index within the round (event slot)         */
+  int32_t send_wait;   /* 1: the sent segment is the previous round's reduce
+                          output for `seg`; wait for it before sending        */
+  int32_t send_buf, recv_buf, red_dst_buf, red_src_buf;
+  int64_t send_off, send_bytes;
+  int64_t recv_off, recv_bytes;
+  int64_t red_dst_off, red_src_off, red_elems;
+};
+
+/* Reduce-scatter plan for one rank.  Round k sends block (rank-1-k) and
+ * receives block (rank-2-k) mod world -- the reference's
+ * rs_send/recv_chunk_index (src/pg.c:141-148) evaluated at rank-1, so that
+ * rank r finishes with block r.  Segments: chunk_elems_from_bytes(chunk_bytes)
+ * (src/pg.c:118-123) elements; blocks <= eager_max bytes are one segment;
+ * `inflight` segments per batch.  out_aliases_src: OUT is block `rank` of
+ * SRC (in-place all-reduce).  Returns the number of steps written (or needed,
+ * when steps == NULL), -1 on bad arguments. */
+int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
+                           size_t chunk_bytes, size_t eager_max, int inflight,
+                           int out_aliases_src, struct pg_step *steps, int max_steps);
+
+/* All-gather plan: round k sends block (rank-k) and receives block
+ * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole blocks, no reduce.
+ * uniform = 1: blocks of `count` elements (pg_all_gather);
+ * uniform = 0: the reduce-scatter partition of `count` (pg_all_reduce). */
+int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform,
+                       struct pg_step *steps, int max_steps);
+
+/* Open a handle without a server list: transport LOOPBACK (reference mock
+ * semantics for a given rank/world) or SELF (world must be 1).  The device is
+ * the current HIP device. */
+int pg_connect_local(int rank, int world, int transport, void **out_handle);
+
+/* Run one collective over `world` virtual ranks in this process (transport
+ * THREADS): rank r uses sendbufs[r] / recvbufs[r] (HIP device or host
+ * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce. */
+#define PG_COLL_REDUCE_SCATTER 0
+#define PG_COLL_ALL_GATHER     1
+#define PG_COLL_ALL_REDUCE     2
+int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbufs,
+                int count, int datatype, int op, size_t chunk_bytes,
+                size_t eager_max, int inflight);
+
+/* Measurements of the last collective on this handle. */
+struct pg_stats {
+  double wall_us;        /* host wall time of the call                      */
+  double h2d_us, d2h_us; /* host-staging copies (0 when device-resident)    */
+  double ring_us;        /* device part: first transfer to last reduce      */
+  int64_t reduce_launches;
+  int64_t reduce_elems;  /* elements reduced by this rank                   */
+  int64_t bytes_sent, bytes_recv;
+};
+int pg_get_stats(void *pg_handle, struct pg_stats *out);
+
+/* Last error message of the calling thread ("" if none). */
+const char *pg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PG_EXT_H */

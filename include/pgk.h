@@ -1,0 +1,69 @@
+/*
+ * include/pgk.h -- thin C-ABI from the host schedule to the MI355X (gfx950)
+ * reduction kernels.  Plain pointers and sizes only; no HIP or torch types.
+ *
+ * This is the inner boundary of the drop-in: the reference's
+ *   static void reduce_inplace(void *dst, const void *src, size_t n,
+ *                              DATATYPE dt, OPERATION op)        (src/pg.c:151-159)
+ * called once per arriving segment by pg_sendrecv_mock (src/pg.c:166-179, call
+ * at :172) becomes pgk_reduce(), called once per arriving segment by the ring
+ * executor in libpg_amd.so.
+ *
+ * All device pointers are HIP device (or managed) allocations on the current
+ * device.  `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ * Calls are asynchronous on `stream`, allocate nothing and are safe to capture
+ * into a hipGraph.  Return 0 on success, -1 on failure (message via
+ * pgk_last_error()).
+ */
+#ifndef PGK_H
+#define PGK_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same values as DATATYPE / OPERATION in include/pg.h (reference pg.h:78-87). */
+#define PGK_DT_INT32  0
+#define PGK_DT_DOUBLE 1
+#define PGK_OP_SUM    0
+#define PGK_OP_PROD   1
+
+/* dst[i] = dst[i] op src[i] for i < n.  Replaces reduce_inplace
+ * (reference src/pg.c:151-159): int32 wraps (two's complement), double is one
+ * IEEE-754 add or multiply per element (round-to-nearest, denormals kept), so
+ * results are bit-identical to the reference loop for every non-NaN result.
+ * dst and src must not partially overlap (dst == src is allowed).
+ * n == 0 is a no-op returning 0.  dt/op outside the values above -> -1. */
+int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *stream);
+
+/* out[i] = a[i] op b[i] (out may equal a or b).  Same numerics as pgk_reduce;
+ * used where the ring must not modify the caller's send buffer. */
+int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
+                   void *stream);
+
+/* Device helpers for hosts that do not link HIP themselves (ctypes, cgo ...). */
+int pgk_device_count(int *count);
+int pgk_set_device(int device);
+int pgk_synchronize(void);
+
+/* Launch tuning, process-wide.  blocks_per_cu: grid cap = CUs x blocks_per_cu
+ * (0 = uncapped one-shot grid, <0 = keep).  nontemporal: 1 = nt loads/stores,
+ * 0 = default cache policy, <0 = keep.  Defaults are the measured best
+ * (DESIGN.md). */
+int pgk_tune(int blocks_per_cu, int nontemporal);
+
+/* Grid the next pgk_reduce of n elements of dt would launch (for bench/tests). */
+int pgk_launch_geometry(size_t n, int dt, unsigned *grid, unsigned *block);
+
+/* Last error message of the calling thread ("" if none). */
+const char *pgk_last_error(void);
+
+/* Build identification, e.g. "pgk gfx950 hip-7.2". */
+const char *pgk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGK_H */

@@ -1,0 +1,504 @@
+/*
+ * pg.c -- public API of libpg_amd.so (include/pg.h): handle lifecycle,
+ * argument validation, host<->HBM staging, and dispatch to
+ *   SELF      world_size == 1: the reference's copy fast paths
+ *             (src/pg.c:269-272, :302-306, :328-330)
+ *   LOOPBACK  the reference's single-process mock schedule
+ *             (src/pg.c:264-321), every reduce on the gfx950 kernel
+ *   ring      RCCL over xGMI (or in-process virtual ranks): pg_plan.c's
+ *             schedule executed by pg_exec.c
+ *
+ * Validation and return codes follow the reference exactly
+ * (src/pg.c:267, :295, :325): NULL handle/buffer, count < 0 or an unknown
+ * datatype -> -1.  An operation other than OP_SUM multiplies, as the
+ * reference's `(op == OP_SUM) ? add : mul` does (src/pg.c:154,157).
+ */
+#define _GNU_SOURCE
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "pg_impl.h"
+
+/* ---- errors ----------------------------------------------------------------- */
+
+static __thread char g_pg_err[512];
+
+void pg_set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_pg_err, sizeof(g_pg_err), fmt, ap);
+  va_end(ap);
+  if (getenv("PG_DEBUG")) fprintf(stderr, "[pg] %s\n", g_pg_err);
+}
+
+const char *pg_last_error(void) { return g_pg_err; }
+
+/* ---- small helpers ---------------------------------------------------------- */
+
+size_t pg_elem_size(int dt) {                 /* reference src/pg.c:109-115 */
+  return dt == DT_INT32 ? 4 : dt == DT_DOUBLE ? 8 : 0;
+}
+
+static double now_us(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
+}
+
+int pg_ensure(void **buf, size_t *cap, size_t bytes) {
+  if (bytes <= *cap && (*buf || bytes == 0)) return 0;
+  if (*buf) { hipFree(*buf); *buf = NULL; *cap = 0; }
+  size_t want = (bytes + 0xFFFFF) & ~(size_t)0xFFFFF;     /* 1 MiB granules */
+  PG_CHECK_HIP(hipMalloc(buf, want));
+  *cap = want;
+  return 0;
+}
+
+/* HIP device or managed memory?  Anything else is treated as host memory and
+ * staged through HBM. */
+static int is_device_ptr(const void *p) {
+  if (!p) return 0;
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof(a));
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
+}
+
+static int ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+  const char *x = (const char *)a, *y = (const char *)b;
+  return na && nb && x < y + nb && y < x + na;
+}
+
+static int copy_any(void *dst, const void *src, size_t bytes) {
+  if (!bytes || dst == src) return 0;
+  if (!is_device_ptr(dst) && !is_device_ptr(src)) { memmove(dst, src, bytes); return 0; }
+  PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  return 0;
+}
+
+static int timed_copy(void *dst, const void *src, size_t bytes, double *acc_us) {
+  double t = now_us();
+  int rc = copy_any(dst, src, bytes);
+  *acc_us += now_us() - t;
+  return rc;
+}
+
+/* ---- handle ----------------------------------------------------------------- */
+
+int pg_impl_create(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)calloc(1, sizeof(*im));
+  if (!im) { pg_set_error("out of host memory"); return -1; }
+  pg->impl = im;
+  im->pg = pg;
+  PG_CHECK_HIP(hipSetDevice(pg->device));
+  PG_CHECK_HIP(hipStreamCreateWithFlags(&im->comm, hipStreamNonBlocking));
+  PG_CHECK_HIP(hipStreamCreateWithFlags(&im->red, hipStreamNonBlocking));
+  for (int i = 0; i < PG_RECV_EVENTS; ++i)
+    PG_CHECK_HIP(hipEventCreateWithFlags(&im->recv_ev[i], hipEventDisableTiming));
+  PG_CHECK_HIP(hipEventCreateWithFlags(&im->join_ev, hipEventDisableTiming));
+  PG_CHECK_HIP(hipEventCreate(&im->t0));
+  PG_CHECK_HIP(hipEventCreate(&im->t1));
+  return 0;
+}
+
+void pg_impl_destroy(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  if (!im) return;
+  if (im->comm) hipStreamSynchronize(im->comm);
+  if (im->red) hipStreamSynchronize(im->red);
+  if (im->ops && im->ops->destroy) im->ops->destroy(im);
+  for (int i = 0; i < im->n_red_ev; ++i) hipEventDestroy(im->red_ev[i]);
+  free(im->red_ev);
+  for (int i = 0; i < PG_RECV_EVENTS; ++i) if (im->recv_ev[i]) hipEventDestroy(im->recv_ev[i]);
+  if (im->join_ev) hipEventDestroy(im->join_ev);
+  if (im->t0) hipEventDestroy(im->t0);
+  if (im->t1) hipEventDestroy(im->t1);
+  if (im->comm) hipStreamDestroy(im->comm);
+  if (im->red) hipStreamDestroy(im->red);
+  for (int i = 0; i < 2; ++i) if (im->stage[i]) hipFree(im->stage[i]);
+  if (im->dsrc) hipFree(im->dsrc);
+  if (im->dout) hipFree(im->dout);
+  free(im->steps);
+  free(im);
+  pg->impl = NULL;
+}
+
+static void pg_defaults(struct pg *pg) {
+  pg->chunk_bytes = PG_DEFAULT_CHUNK_BYTES;
+  pg->eager_max = PG_DEFAULT_EAGER_MAX;
+  pg->inflight = PG_DEFAULT_INFLIGHT;
+  pg->port = PG_DEFAULT_PORT;
+  pg_apply_env(pg);                 /* env after defaults: env wins */
+}
+
+int connect_process_group(const char *serverlist, void **out_handle) {
+  if (!serverlist || !out_handle) { pg_set_error("connect_process_group: NULL argument"); return -1; }
+  struct pg *pg = (struct pg *)calloc(1, sizeof(*pg));
+  if (!pg) return -1;
+  if (pg_parse_hosts(serverlist, &pg->hosts, &pg->world_size)) goto fail;
+  if (pg_discover_rank(pg->hosts, pg->world_size, &pg->rank)) goto fail;
+  pg_defaults(pg);
+  if (pg_discover_device(pg->rank, &pg->device)) goto fail;
+
+  const char *tr = getenv("PG_TRANSPORT");
+  if (pg->world_size == 1) pg->transport = PG_TRANSPORT_SELF;
+  else if (tr && strcmp(tr, "loopback") == 0) pg->transport = PG_TRANSPORT_LOOPBACK;
+  else if (!tr || !*tr || strcmp(tr, "rccl") == 0) pg->transport = PG_TRANSPORT_RCCL;
+  else { pg_set_error("PG_TRANSPORT=%s: expected rccl or loopback", tr); goto fail; }
+
+  if (pg_impl_create(pg)) goto fail;
+  if (pg->transport == PG_TRANSPORT_RCCL && pg_xport_rccl_init(pg)) goto fail;
+  *out_handle = pg;
+  return 0;
+fail:
+  fprintf(stderr, "Process group connection failed during setup: %s\n", pg_last_error());
+  pg_close(pg);
+  return -1;
+}
+
+int pg_connect_local(int rank, int world, int transport, void **out_handle) {
+  if (!out_handle || world < 1 || rank < 0 || rank >= world) { pg_set_error("pg_connect_local: bad arguments"); return -1; }
+  if (transport != PG_TRANSPORT_LOOPBACK && transport != PG_TRANSPORT_SELF) {
+    pg_set_error("pg_connect_local: transport must be LOOPBACK or SELF");
+    return -1;
+  }
+  if (transport == PG_TRANSPORT_SELF && world != 1) { pg_set_error("pg_connect_local: SELF needs world 1"); return -1; }
+  struct pg *pg = (struct pg *)calloc(1, sizeof(*pg));
+  if (!pg) return -1;
+  pg->rank = rank;
+  pg->world_size = world;
+  pg_defaults(pg);
+  if (hipGetDevice(&pg->device) != hipSuccess) { pg_set_error("no HIP device"); free(pg); return -1; }
+  pg->transport = world == 1 ? PG_TRANSPORT_SELF : transport;
+  if (pg_impl_create(pg)) { pg_close(pg); return -1; }
+  *out_handle = pg;
+  return 0;
+}
+
+int pg_close(void *pg_handle) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg) return 0;
+  pg_impl_destroy(pg);
+  if (pg->hosts) {
+    for (int i = 0; i < pg->world_size; ++i) free(pg->hosts[i]);
+    free(pg->hosts);
+  }
+  free(pg);
+  return 0;
+}
+
+int pg_get_stats(void *pg_handle, struct pg_stats *out) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg || !pg->impl || !out) return -1;
+  *out = ((struct pg_impl *)pg->impl)->stats;
+  return 0;
+}
+
+static void stats_begin(struct pg_impl *im) { memset(&im->stats, 0, sizeof(im->stats)); }
+
+static int sync_ring(struct pg_impl *im, int timed) {
+  PG_CHECK_HIP(hipStreamSynchronize(im->comm));
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (timed) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
+  }
+  return 0;
+}
+
+static int plan_into(struct pg_impl *im, int is_rs, int count, int dt, int alias, int uniform) {
+  struct pg *pg = im->pg;
+  int n = is_rs ? pg_plan_reduce_scatter(pg->rank, pg->world_size, count, dt, pg->chunk_bytes,
+                                         pg->eager_max, pg->inflight, alias, NULL, 0)
+                : pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, NULL, 0);
+  if (n < 0) { pg_set_error("plan: bad arguments"); return -1; }
+  if (n > im->steps_cap) {
+    struct pg_step *s = (struct pg_step *)realloc(im->steps, sizeof(*s) * (size_t)n);
+    if (!s) { pg_set_error("plan: out of host memory"); return -1; }
+    im->steps = s;
+    im->steps_cap = n;
+  }
+  if (is_rs)
+    pg_plan_reduce_scatter(pg->rank, pg->world_size, count, dt, pg->chunk_bytes, pg->eager_max,
+                           pg->inflight, alias, im->steps, im->steps_cap);
+  else
+    pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, im->steps, im->steps_cap);
+  return n;
+}
+
+static int ensure_stage(struct pg_impl *im, int count, int dt) {
+  size_t blk = ((size_t)count + (size_t)im->pg->world_size - 1) / (size_t)im->pg->world_size;
+  size_t bytes = blk * pg_elem_size(dt);
+  size_t cap1 = im->stage_cap;
+  if (pg_ensure(&im->stage[0], &im->stage_cap, bytes)) return -1;
+  return pg_ensure(&im->stage[1], &cap1, bytes);
+}
+
+/* ---- reduce-scatter ---------------------------------------------------------- */
+
+static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  size_t es = pg_elem_size(dt), boff, blen;
+  pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
+  int sd = is_device_ptr(sendbuf), rd = is_device_ptr(recvbuf);
+  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());   /* caller's producers */
+
+  void *src = sendbuf;
+  if (!sd) {
+    if (pg_ensure(&im->dsrc, &im->dsrc_cap, (size_t)count * es)) return -1;
+    if (timed_copy(im->dsrc, sendbuf, (size_t)count * es, &im->stats.h2d_us)) return -1;
+    src = im->dsrc;
+  }
+  void *out = recvbuf;
+  int post_copy = 0;
+  if (!rd || ranges_overlap(recvbuf, blen * es, src, (size_t)count * es)) {
+    if (pg_ensure(&im->dout, &im->dout_cap, blen * es)) return -1;
+    out = im->dout;
+    post_copy = 1;
+  }
+  if (ensure_stage(im, count, dt)) return -1;
+  int n = plan_into(im, 1, count, dt, 0, 0);
+  if (n < 0) return -1;
+  void *bufs[5] = {NULL, src, out, im->stage[0], im->stage[1]};
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  if (pg_exec_plan(im, im->steps, n, bufs, dt, op)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
+  if (sync_ring(im, 1)) return -1;
+  if (post_copy && timed_copy(recvbuf, out, blen * es, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+/* The reference's mock (src/pg.c:264-291) on the GPU: recvbuf is indexed as a
+ * full count-element buffer and the partition unit is chunk_bytes. */
+static int loopback_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  size_t es = pg_elem_size(dt), bytes = (size_t)count * es;
+  size_t ce = pg->chunk_bytes / es ? pg->chunk_bytes / es : 1;      /* src/pg.c:118-123 */
+  int W = pg->world_size, r = pg->rank;
+  /* refuse the shapes where the reference reads past sendbuf (src/pg.c:282-287
+   * use recv_len on the send side): on a GPU that read could fault */
+  for (int k = 0; k + 1 < W; ++k) {
+    size_t s_idx = (size_t)(((r - k) % W + W) % W), r_idx = (size_t)(((r - k - 1) % W + W) % W);
+    size_t so = s_idx * ce, ro = r_idx * ce;
+    size_t rl = ro < (size_t)count ? (((ro + ce) < (size_t)count ? ro + ce : (size_t)count) - ro) : 0;
+    if (rl && so + rl > (size_t)count) {
+      pg_set_error("loopback reduce_scatter: the reference reads past sendbuf for this shape "
+                   "(count=%d chunk_elems=%zu rank=%d world=%d)", count, ce, r, W);
+      return -1;
+    }
+  }
+  int sd = is_device_ptr(sendbuf), rd = is_device_ptr(recvbuf);
+  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());
+  char *s, *d;
+  if (sendbuf == recvbuf) {
+    if (rd) s = d = (char *)recvbuf;
+    else {
+      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+      s = d = (char *)im->dout;
+    }
+  } else {
+    if (sd) s = (char *)sendbuf;
+    else {
+      if (pg_ensure(&im->dsrc, &im->dsrc_cap, bytes) || timed_copy(im->dsrc, sendbuf, bytes, &im->stats.h2d_us)) return -1;
+      s = (char *)im->dsrc;
+    }
+    if (rd) d = (char *)recvbuf;
+    else {
+      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+      d = (char *)im->dout;
+    }
+  }
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
+  for (int k = 0; k + 1 < W; ++k) {                       /* src/pg.c:277-289 */
+    size_t s_idx = (size_t)(((r - k) % W + W) % W), r_idx = (size_t)(((r - k - 1) % W + W) % W);
+    size_t so = s_idx * ce, ro = r_idx * ce;
+    if (ro >= (size_t)count) continue;                     /* recv_len == 0 */
+    size_t rend = ro + ce < (size_t)count ? ro + ce : (size_t)count;
+    /* lengths are whole elements, so the mock's tail memcpy (:174-177) never runs */
+    if (pgk_reduce(d + ro * es, s + so * es, rend - ro, dt, op, (void *)im->red)) {
+      pg_set_error("%s", pgk_last_error());
+      return -1;
+    }
+    im->stats.reduce_launches++;
+    im->stats.reduce_elems += (int64_t)(rend - ro);
+  }
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->red));
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
+  if (!rd && timed_copy(recvbuf, d, bytes, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype,
+                      OPERATION op, void *pg_handle) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg || !sendbuf || !recvbuf || count < 0 || pg_elem_size(datatype) == 0) {
+    pg_set_error("pg_reduce_scatter: invalid argument");
+    return -1;                                               /* src/pg.c:267 */
+  }
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  if (!im) { pg_set_error("pg_reduce_scatter: closed handle"); return -1; }
+  int kop = op == OP_SUM ? PGK_OP_SUM : PGK_OP_PROD;
+  double t = now_us();
+  stats_begin(im);
+  int rc;
+  if (pg->world_size == 1)                                  /* src/pg.c:269-272 */
+    rc = copy_any(recvbuf, sendbuf, (size_t)count * pg_elem_size(datatype));
+  else if (pg->transport == PG_TRANSPORT_LOOPBACK)
+    rc = loopback_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  else
+    rc = ring_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  im->stats.wall_us = now_us() - t;
+  return rc;
+}
+
+/* ---- all-gather ---------------------------------------------------------------- */
+
+static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)pg->world_size;
+  int rd = is_device_ptr(recvbuf), sd = sendbuf && is_device_ptr(sendbuf);
+  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  char *full = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
+    full = (char *)im->dout;
+  }
+  char *own = full + (size_t)pg->rank * slot;
+  if (sendbuf) {
+    if ((char *)sendbuf != own && timed_copy(own, sendbuf, slot, sd ? &im->stats.ring_us : &im->stats.h2d_us)) return -1;
+  } else if (!rd) {
+    if (timed_copy(own, (char *)recvbuf + (size_t)pg->rank * slot, slot, &im->stats.h2d_us)) return -1;
+  }
+  int n = plan_into(im, 0, count, dt, 0, 1);
+  if (n < 0) return -1;
+  void *bufs[5] = {NULL, NULL, full, NULL, NULL};
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  if (pg_exec_plan(im, im->steps, n, bufs, dt, PGK_OP_SUM)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
+  if (sync_ring(im, 1)) return -1;
+  if (!rd && timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+/* The reference's mock all-gather (src/pg.c:293-321): it SUMS slot (r-k) into
+ * slot (r-k-1) instead of copying (:317).  Reproduced for parity only. */
+static int loopback_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  int W = pg->world_size, r = pg->rank;
+  size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)W;
+  int rd = is_device_ptr(recvbuf), sd = sendbuf && is_device_ptr(sendbuf);
+  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  char *full = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, total) || timed_copy(im->dout, recvbuf, total, &im->stats.h2d_us)) return -1;
+    full = (char *)im->dout;
+  }
+  if (sendbuf && timed_copy(full + (size_t)r * slot, sendbuf, slot, &im->stats.h2d_us)) return -1;
+  for (int k = 0; k + 1 < W; ++k) {
+    int s = ((r - k) % W + W) % W, d = ((r - k - 1) % W + W) % W;
+    if (pgk_reduce(full + (size_t)d * slot, full + (size_t)s * slot, (size_t)count, dt, PGK_OP_SUM,
+                   (void *)im->red)) {
+      pg_set_error("%s", pgk_last_error());
+      return -1;
+    }
+    im->stats.reduce_launches++;
+  }
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (!rd && timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, void *pg_handle) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg || !recvbuf || count < 0 || pg_elem_size(datatype) == 0) {
+    pg_set_error("pg_all_gather: invalid argument");
+    return -1;                                               /* src/pg.c:295 */
+  }
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  if (!im) { pg_set_error("pg_all_gather: closed handle"); return -1; }
+  double t = now_us();
+  stats_begin(im);
+  int rc;
+  if (pg->world_size == 1)                                  /* src/pg.c:302-306 */
+    rc = sendbuf ? copy_any(recvbuf, sendbuf, (size_t)count * pg_elem_size(datatype)) : 0;
+  else if (pg->transport == PG_TRANSPORT_LOOPBACK)
+    rc = loopback_all_gather(pg, sendbuf, recvbuf, count, datatype);
+  else
+    rc = ring_all_gather(pg, sendbuf, recvbuf, count, datatype);
+  im->stats.wall_us = now_us() - t;
+  return rc;
+}
+
+/* ---- all-reduce ------------------------------------------------------------------ */
+
+/* Reduce-scatter in place on the working copy, then all-gather it: the
+ * reference's composition (src/pg.c:323-339) on one full-size buffer, without
+ * its out-of-bounds all-gather sizing (:303, :313-317). */
+static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  size_t es = pg_elem_size(dt), bytes = (size_t)count * es, boff, blen;
+  pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
+  int rd = is_device_ptr(recvbuf), sd = is_device_ptr(sendbuf);
+  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  char *work = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
+    work = (char *)im->dout;
+  }
+  if (sendbuf != recvbuf) {
+    if (timed_copy(work, sendbuf, bytes, sd ? &im->stats.ring_us : &im->stats.h2d_us)) return -1;
+  } else if (!rd) {
+    if (timed_copy(work, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+  }
+  if (ensure_stage(im, count, dt)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  int n = plan_into(im, 1, count, dt, 1, 0);
+  if (n < 0) return -1;
+  void *rs_bufs[5] = {NULL, work, work + boff * es, im->stage[0], im->stage[1]};
+  if (pg_exec_plan(im, im->steps, n, rs_bufs, dt, op)) return -1;
+  n = plan_into(im, 0, count, dt, 0, 0);
+  if (n < 0) return -1;
+  void *ag_bufs[5] = {NULL, NULL, work, NULL, NULL};
+  if (pg_exec_plan(im, im->steps, n, ag_bufs, dt, op)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
+  if (sync_ring(im, 1)) return -1;
+  if (!rd && timed_copy(recvbuf, work, bytes, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OPERATION op,
+                  void *pg_handle) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg || !sendbuf || !recvbuf || count < 0) {
+    pg_set_error("pg_all_reduce: invalid argument");
+    return -1;                                               /* src/pg.c:325 */
+  }
+  if (pg_elem_size(datatype) == 0) {                         /* via RS, src/pg.c:333 */
+    pg_set_error("pg_all_reduce: unknown datatype %d", (int)datatype);
+    return -1;
+  }
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  if (!im) { pg_set_error("pg_all_reduce: closed handle"); return -1; }
+  int kop = op == OP_SUM ? PGK_OP_SUM : PGK_OP_PROD;
+  double t = now_us();
+  stats_begin(im);
+  int rc;
+  if (pg->world_size == 1)                                  /* src/pg.c:328-330 */
+    rc = sendbuf != recvbuf ? copy_any(recvbuf, sendbuf, (size_t)count * pg_elem_size(datatype)) : 0;
+  else if (pg->transport == PG_TRANSPORT_LOOPBACK) {
+    pg_set_error("pg_all_reduce: the reference's world_size > 1 all-reduce writes past a "
+                 "count-element recvbuf (src/pg.c:303,313-317); no defined result to reproduce");
+    rc = -1;
+  } else
+    rc = ring_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
+  im->stats.wall_us = now_us() - t;
+  return rc;
+}

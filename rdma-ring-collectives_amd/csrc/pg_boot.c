@@ -1,0 +1,212 @@
+/*
+ * pg_boot.c -- server list, rank/device discovery, tuning env, and the TCP
+ * relay that hands rank 0's RCCL unique id to every other rank.
+ *
+ * Reference counterparts: parse_server_list (src/pg.c:64-102), rank by
+ * gethostname (src/pg.c:188-200), pg_init_env (src/pg.c:40-58) and the TCP
+ * ring bootstrap (src/pg_net.c:721-783) that exchanged queue-pair info.  On
+ * one 8-GPU node the only thing to bootstrap is a 128-byte ncclUniqueId, so
+ * the relay is a star on hosts[0]:port, with the reference's retry/backoff
+ * discipline (src/pg_net.c:298-436) and timeout env names.
+ */
+#define _GNU_SOURCE
+#include <ctype.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/types.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "pg_impl.h"
+
+int pg_parse_hosts(const char *list, char ***hosts_out, int *n_out) {
+  int n = 0, cap = 8;
+  char **hosts = (char **)malloc(sizeof(char *) * (size_t)cap);
+  if (!hosts) return -1;
+  const char *p = list;
+  for (;;) {
+    while (*p && isspace((unsigned char)*p)) ++p;
+    if (!*p) break;
+    const char *q = p;
+    while (*q && !isspace((unsigned char)*q)) ++q;
+    if (n == cap) {
+      cap *= 2;
+      char **h2 = (char **)realloc(hosts, sizeof(char *) * (size_t)cap);
+      if (!h2) goto fail;
+      hosts = h2;
+    }
+    hosts[n] = strndup(p, (size_t)(q - p));
+    if (!hosts[n]) goto fail;
+    ++n;
+    p = q;
+  }
+  if (n == 0) { pg_set_error("connect_process_group: empty server list"); goto fail; }
+  *hosts_out = hosts;
+  *n_out = n;
+  return 0;
+fail:
+  for (int i = 0; i < n; ++i) free(hosts[i]);
+  free(hosts);
+  return -1;
+}
+
+static int env_int(const char *name, int *out) {
+  const char *s = getenv(name);
+  if (!s || !*s) return 0;
+  char *end = NULL;
+  long v = strtol(s, &end, 0);
+  if (end == s) return 0;
+  *out = (int)v;
+  return 1;
+}
+
+int pg_discover_rank(char **hosts, int n, int *rank_out) {
+  int r;
+  if (env_int("PG_RANK", &r) || env_int("RANK", &r)) {
+    if (r < 0 || r >= n) {
+      pg_set_error("rank %d from PG_RANK/RANK outside server list of %d", r, n);
+      return -1;
+    }
+    *rank_out = r;
+    return 0;
+  }
+  char self[256];
+  if (gethostname(self, sizeof(self)) != 0) {
+    pg_set_error("gethostname: %s", strerror(errno));
+    return -1;
+  }
+  self[sizeof(self) - 1] = 0;
+  for (int i = 0; i < n; ++i)
+    if (strcmp(hosts[i], self) == 0) { *rank_out = i; return 0; }
+  pg_set_error("Hostname '%s' not found in server list (set PG_RANK)", self);
+  return -1;
+}
+
+int pg_discover_device(int rank, int *device_out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    pg_set_error("no HIP device visible");
+    return -1;
+  }
+  int d;
+  if (env_int("PG_DEVICE", &d) || env_int("LOCAL_RANK", &d)) {
+    if (d < 0 || d >= ndev) { pg_set_error("device %d out of range (%d devices)", d, ndev); return -1; }
+  } else {
+    d = rank % ndev;
+  }
+  *device_out = d;
+  return 0;
+}
+
+void pg_apply_env(struct pg *pg) {
+  const char *s;
+  if ((s = getenv("PG_CHUNK_BYTES")) && *s) {
+    unsigned long long v = strtoull(s, NULL, 0);
+    if (v) pg->chunk_bytes = (size_t)v;
+  }
+  if ((s = getenv("PG_EAGER_MAX")) && *s) pg->eager_max = (size_t)strtoull(s, NULL, 0);
+  int v;
+  if (env_int("PG_INFLIGHT", &v) && v > 0) pg->inflight = v;
+  if (env_int("PG_PORT", &v) && v > 0 && v < 65536) pg->port = v;
+}
+
+static long now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+static int io_full(int fd, void *buf, size_t n, int writing) {
+  char *p = (char *)buf;
+  while (n) {
+    ssize_t k = writing ? send(fd, p, n, MSG_NOSIGNAL) : recv(fd, p, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return -1;
+    p += k;
+    n -= (size_t)k;
+  }
+  return 0;
+}
+
+/* Rank 0 serves `blob` to every other rank over TCP; the others fetch it. */
+int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes) {
+  int timeout_ms = PG_DEFAULT_CONNECT_TIMEOUT_MS, backoff_ms = PG_DEFAULT_BACKOFF_MS;
+  env_int("PG_CONNECT_TIMEOUT_MS", &timeout_ms);
+  env_int("PG_BACKOFF_MS", &backoff_ms);
+  char port[16];
+  snprintf(port, sizeof(port), "%d", pg->port);
+
+  if (pg->rank == 0) {
+    int ls = socket(AF_INET, SOCK_STREAM, 0);
+    if (ls < 0) { pg_set_error("socket: %s", strerror(errno)); return -1; }
+    int one = 1;
+    setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    struct sockaddr_in a;
+    memset(&a, 0, sizeof(a));
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    a.sin_port = htons((uint16_t)pg->port);
+    if (bind(ls, (struct sockaddr *)&a, sizeof(a)) || listen(ls, pg->world_size)) {
+      pg_set_error("bootstrap listen on port %d: %s", pg->port, strerror(errno));
+      close(ls);
+      return -1;
+    }
+    long deadline = now_ms() + timeout_ms;
+    int served = 0;
+    while (served < pg->world_size - 1) {
+      struct pollfd pfd = {ls, POLLIN, 0};
+      long left = deadline - now_ms();
+      if (left <= 0) { pg_set_error("bootstrap: %d of %d ranks never connected", pg->world_size - 1 - served, pg->world_size - 1); close(ls); return -1; }
+      int pr = poll(&pfd, 1, (int)left);
+      if (pr < 0 && errno == EINTR) continue;
+      if (pr <= 0) continue;
+      int c = accept(ls, NULL, NULL);
+      if (c < 0) continue;
+      int32_t peer = -1;
+      if (io_full(c, &peer, sizeof(peer), 0) == 0 && peer > 0 && peer < pg->world_size &&
+          io_full(c, blob, blob_bytes, 1) == 0) {
+        uint8_t ack = 0;
+        if (io_full(c, &ack, 1, 0) == 0 && ack == 0xA5) ++served;  /* ready token, cf. pg_net.c:699-710 */
+      }
+      close(c);
+    }
+    close(ls);
+    return 0;
+  }
+
+  struct addrinfo hints, *res = NULL;
+  memset(&hints, 0, sizeof(hints));
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  int gai = getaddrinfo(pg->hosts[0], port, &hints, &res);
+  if (gai != 0 || !res) { pg_set_error("bootstrap: resolve %s: %s", pg->hosts[0], gai_strerror(gai)); return -1; }
+  long deadline = now_ms() + timeout_ms;
+  int rc = -1;
+  while (now_ms() < deadline) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) break;
+    if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+      int32_t me = pg->rank;
+      uint8_t ack = 0xA5;
+      if (io_full(fd, &me, sizeof(me), 1) == 0 && io_full(fd, blob, blob_bytes, 0) == 0 &&
+          io_full(fd, &ack, 1, 1) == 0) {
+        rc = 0;
+        close(fd);
+        break;
+      }
+    }
+    close(fd);
+    struct timespec ts = {backoff_ms / 1000, (long)(backoff_ms % 1000) * 1000000L};
+    nanosleep(&ts, NULL);
+  }
+  freeaddrinfo(res);
+  if (rc) pg_set_error("bootstrap: could not reach rank 0 at %s:%s within %d ms", pg->hosts[0], port, timeout_ms);
+  return rc;
+}

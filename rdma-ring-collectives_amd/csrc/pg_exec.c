@@ -1,0 +1,111 @@
+/*
+ * pg_exec.c -- executes a ring plan (pg_plan.c) on one rank.
+ *
+ * Two HIP streams per rank:
+ *   comm : transport groups (RCCL ncclSend/ncclRecv over xGMI), in plan order
+ *   red  : pgk_reduce of each arrived segment
+ * and two kinds of events:
+ *   recv_ev[batch]  comm -> red : the batch's segments have landed
+ *   red_ev[seg]     red -> comm : the segment's partial is reduced and may be
+ *                                 forwarded in the next round
+ * so segment j of round k+1 is on the wire while segment j+1 of round k is
+ * still being reduced.  This is the pipelining that the reference describes
+ * for its RDMA path (README.md:17,74-77) and mocks with one synchronous local
+ * call per chunk (src/pg.c:276-289).
+ *
+ * Buffer reuse is safe by construction: a staging segment is overwritten by a
+ * receive two rounds later, which the comm stream orders after the send of
+ * the intervening round, and that send waited on the segment's reduce.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pg_impl.h"
+
+static int ensure_red_events(struct pg_impl *im, int need) {
+  if (need <= im->n_red_ev) return 0;
+  int cap = im->n_red_ev ? im->n_red_ev : 16;
+  while (cap < need) cap *= 2;
+  hipEvent_t *ev = (hipEvent_t *)realloc(im->red_ev, sizeof(hipEvent_t) * (size_t)cap);
+  if (!ev) { pg_set_error("pg_exec: out of host memory"); return -1; }
+  im->red_ev = ev;
+  for (int i = im->n_red_ev; i < cap; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&im->red_ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      im->n_red_ev = i;
+      pg_set_error("pg_exec: hipEventCreate: %s", hipGetErrorString(e));
+      return -1;
+    }
+  }
+  im->n_red_ev = cap;
+  return 0;
+}
+
+static inline char *at(void *const bufs[5], int which, int64_t off) {
+  return (char *)bufs[which] + off;
+}
+
+int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
+                 void *const bufs[5], int dt, int op) {
+  if (n <= 0) return 0;
+  const struct pg *pg = im->pg;
+  const int right = (pg->rank + 1) % pg->world_size;
+  const int left = (pg->rank - 1 + pg->world_size) % pg->world_size;
+
+  int max_seg = 0;
+  for (int i = 0; i < n; ++i) if (st[i].seg > max_seg) max_seg = st[i].seg;
+  if (ensure_red_events(im, max_seg + 1)) return -1;
+
+  int i = 0, nb = 0;
+  while (i < n) {
+    int b = st[i].batch, j = i;
+    while (j < n && st[j].batch == b) ++j;          /* steps [i, j) = one batch */
+
+    /* forwarded partials must be reduced before they go on the wire */
+    for (int s = i; s < j; ++s)
+      if (st[s].send_bytes && st[s].send_wait)
+        PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->red_ev[st[s].seg], 0));
+
+    if (im->ops->group_start(im)) return -1;
+    for (int s = i; s < j; ++s) {
+      if (st[s].send_bytes &&
+          im->ops->send(im, at(bufs, st[s].send_buf, st[s].send_off), (size_t)st[s].send_bytes,
+                        right, im->comm))
+        return -1;
+      if (st[s].recv_bytes &&
+          im->ops->recv(im, at(bufs, st[s].recv_buf, st[s].recv_off), (size_t)st[s].recv_bytes,
+                        left, im->comm))
+        return -1;
+      im->stats.bytes_sent += st[s].send_bytes;
+      im->stats.bytes_recv += st[s].recv_bytes;
+    }
+    if (im->ops->group_end(im, im->comm)) return -1;
+
+    int any_red = 0;
+    for (int s = i; s < j; ++s) any_red |= st[s].red_elems > 0;
+    if (any_red) {
+      hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
+      PG_CHECK_HIP(hipEventRecord(rev, im->comm));
+      PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
+      for (int s = i; s < j; ++s) {
+        if (!st[s].red_elems) continue;
+        if (pgk_reduce(at(bufs, st[s].red_dst_buf, st[s].red_dst_off),
+                       at(bufs, st[s].red_src_buf, st[s].red_src_off),
+                       (size_t)st[s].red_elems, dt, op, (void *)im->red)) {
+          pg_set_error("pg_exec: %s", pgk_last_error());
+          return -1;
+        }
+        PG_CHECK_HIP(hipEventRecord(im->red_ev[st[s].seg], im->red));
+        im->stats.reduce_launches += 1;
+        im->stats.reduce_elems += st[s].red_elems;
+      }
+    }
+    ++nb;
+    i = j;
+  }
+  /* join: the comm stream observes the last reduce */
+  PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
+  return 0;
+}

@@ -1,0 +1,104 @@
+/*
+ * pg_impl.h -- internals of libpg_amd.so (not installed).
+ *
+ * Layering (mirrors the reference's L3/L2/L1 split):
+ *   pg.c          public API, validation, host<->HBM staging, loopback mock
+ *   pg_plan.c     ring schedule as data (pure C, no HIP)
+ *   pg_exec.c     executes a plan: transport groups on the comm stream,
+ *                 pgk_reduce on the reduce stream, events in between
+ *   pg_xport_*.c  the hop: RCCL P2P over xGMI, or in-process virtual ranks
+ *   pg_boot.c     server list, rank/device discovery, TCP unique-id relay
+ */
+#ifndef PG_IMPL_H
+#define PG_IMPL_H
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pg.h"
+#include "pg_ext.h"
+#include "pgk.h"
+
+/* Defaults.  The reference's 4 KiB chunk (src/constants.h:82) was sized for an
+ * RDMA MTU; a GPU ring segment below ~1 MiB is launch-bound, so the segment
+ * default is 4 MiB here.  eager_max and inflight keep the reference values
+ * (src/constants.h:75,89).  Env overrides win (the reference applied them
+ * only to zero fields after setting defaults, so they never took effect:
+ * src/pg.c:203-209 vs :42-50). */
+#define PG_DEFAULT_CHUNK_BYTES   (4u << 20)
+#define PG_DEFAULT_EAGER_MAX     4096u
+#define PG_DEFAULT_INFLIGHT      4
+#define PG_DEFAULT_PORT          18515
+#define PG_DEFAULT_CONNECT_TIMEOUT_MS 60000
+#define PG_DEFAULT_BACKOFF_MS    100
+
+#define PG_RECV_EVENTS 8
+
+struct pg_impl;
+
+/* The hop.  A group pairs the sends to the right neighbour with the receives
+ * from the left neighbour of one batch; all are enqueued on `stream`.  Same
+ * per-peer ordering rules as ncclSend/ncclRecv. */
+struct pg_xport_ops {
+  const char *name;
+  int (*group_start)(struct pg_impl *im);
+  int (*send)(struct pg_impl *im, const void *buf, size_t bytes, int peer, hipStream_t s);
+  int (*recv)(struct pg_impl *im, void *buf, size_t bytes, int peer, hipStream_t s);
+  int (*group_end)(struct pg_impl *im, hipStream_t s);
+  void (*destroy)(struct pg_impl *im);
+};
+
+struct pg_impl {
+  struct pg *pg;
+  const struct pg_xport_ops *ops;
+  void *xctx;                 /* ncclComm_t, or the virtual-rank context      */
+
+  hipStream_t comm, red;      /* transfers / reductions                       */
+  hipEvent_t *red_ev;         /* per segment: its reduce finished             */
+  int n_red_ev;
+  hipEvent_t recv_ev[PG_RECV_EVENTS]; /* per batch: its receives landed       */
+  hipEvent_t join_ev, t0, t1;
+
+  /* HBM working memory, grown on demand and kept (288 GB per GPU). */
+  void *stage[2];  size_t stage_cap;
+  void *dsrc;      size_t dsrc_cap;   /* device copy of a host sendbuf        */
+  void *dout;      size_t dout_cap;   /* device result / full buffer          */
+
+  struct pg_step *steps; int steps_cap;
+  struct pg_stats stats;
+};
+
+/* pg.c */
+void pg_set_error(const char *fmt, ...);
+int pg_ensure(void **buf, size_t *cap, size_t bytes);   /* hipMalloc-grow */
+int pg_impl_create(struct pg *pg);                        /* streams/events */
+void pg_impl_destroy(struct pg *pg);
+size_t pg_elem_size(int dt);
+
+/* pg_exec.c: run `n` steps; bufs[] indexed by PG_BUF_*. */
+int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
+                 void *const bufs[5], int dt, int op);
+
+/* pg_xport_rccl.c */
+int pg_xport_rccl_init(struct pg *pg);
+/* pg_xport_threads.c */
+int pg_xport_threads_attach(struct pg *pg, void *hub);
+
+/* pg_boot.c */
+int pg_parse_hosts(const char *list, char ***hosts_out, int *n_out);
+int pg_discover_rank(char **hosts, int n, int *rank_out);
+int pg_discover_device(int rank, int *device_out);
+void pg_apply_env(struct pg *pg);
+int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes);
+
+#define PG_CHECK_HIP(expr)                                                          \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      pg_set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+#endif /* PG_IMPL_H */

@@ -1,0 +1,274 @@
+// pgk_reduce.hip -- CDNA4 (gfx950) element-wise reduction kernels + C-ABI.
+//
+// Replaces the reference's scalar hot loop reduce_inplace (src/pg.c:151-159):
+//     d[i] = (op == OP_SUM) ? d[i] + s[i] : d[i] * s[i]     for int32 / double
+//
+// The op is HBM-bound (1 arithmetic op per 12 B (int32) or 24 B (double) of
+// traffic), so there is no MFMA and no LDS: every lane streams 16-byte vectors
+// (global_load_dwordx4 / global_store_dwordx4), each wave moves 1 KiB per
+// instruction per operand, and each thread keeps kUnroll independent vector
+// pairs in flight to cover HBM latency.  The op and dtype are template
+// parameters, so the per-element `op` test of the reference disappears.
+//
+// Numerics (bit-exact vs the reference loop):
+//   int32  -> uint32 add / mul_lo (two's-complement wrap, what gcc emits)
+//   double -> one v_add_f64 / v_mul_f64 per element, RNE, denormals preserved
+//             (built without -ffast-math / denormal flushing); no FMA is
+//             possible because each element sees exactly one operation.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+
+#include "pgk.h"
+
+namespace {
+
+constexpr int kBlock = 256;   // 4 waves of 64
+constexpr int kUnroll = 4;    // 16-B vectors per operand per thread per iteration
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct VecOf;
+template <> struct VecOf<uint32_t> { using type = u32x4; static constexpr int width = 4; };
+template <> struct VecOf<double> { using type = f64x2; static constexpr int width = 2; };
+
+template <int OP, typename X>
+__device__ __forceinline__ X apply(X a, X b) {
+  if constexpr (OP == PGK_OP_SUM) return a + b;
+  else return a * b;
+}
+
+template <bool NT, typename X>
+__device__ __forceinline__ X ld(const X* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <bool NT, typename X>
+__device__ __forceinline__ void st(X* p, X v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// out = a op b over [head elements | nvec 16-B vectors | tail elements].
+// The vector region starts at element `head` and is 16-B aligned in all three
+// pointers; head/tail (< one vector each) are done by the first threads of
+// block 0.  Grid-strided so the host can cap the grid.
+template <typename T, int OP, bool NT>
+__global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
+                                                       const T* __restrict__ a,
+                                                       const T* __restrict__ b,
+                                                       unsigned head, size_t nvec,
+                                                       unsigned tail) {
+  using V = typename VecOf<T>::type;
+  constexpr int W = VecOf<T>::width;
+  if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+    size_t e = threadIdx.x < head ? threadIdx.x
+                                  : head + nvec * W + (threadIdx.x - head);
+    out[e] = apply<OP>(a[e], b[e]);
+  }
+  V* __restrict__ vo = reinterpret_cast<V*>(out + head);
+  const V* __restrict__ va = reinterpret_cast<const V*>(a + head);
+  const V* __restrict__ vb = reinterpret_cast<const V*>(b + head);
+  const size_t tile = (size_t)kBlock * kUnroll;
+  const size_t stride = (size_t)gridDim.x * tile;
+  size_t i = (size_t)blockIdx.x * tile + threadIdx.x;
+  // full tiles: no bounds checks, kUnroll independent loads per operand
+  for (; i + (kUnroll - 1) * kBlock < nvec; i += stride) {
+    V x[kUnroll], y[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) x[u] = ld<NT>(va + i + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) y[u] = ld<NT>(vb + i + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) st<NT>(vo + i + u * kBlock, apply<OP>(x[u], y[u]));
+  }
+  // the one partial tile (at most one per grid)
+  if (i < nvec) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      size_t j = i + u * kBlock;
+      if (j < nvec) st<NT>(vo + j, apply<OP>(ld<NT>(va + j), ld<NT>(vb + j)));
+    }
+  }
+}
+
+// Fallback when the three pointers are not mutually 16-B congruent (e.g. a
+// segment starting at an odd element of an int32 buffer): element-wise, still
+// coalesced (lane i touches element i).
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(T* __restrict__ out,
+                                                          const T* __restrict__ a,
+                                                          const T* __restrict__ b,
+                                                          size_t n) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    out[i] = apply<OP>(a[i], b[i]);
+}
+
+// ---- host side ---------------------------------------------------------------
+
+thread_local char g_err[256] = "";
+
+void set_err(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// Tuning (process-wide).  Measured on MI355X: see DESIGN.md "Kernel tuning".
+int g_blocks_per_cu = 8;
+int g_nontemporal = 1;
+
+constexpr int kMaxDevices = 64;
+int g_cu_count[kMaxDevices];  // 0 = not queried yet
+
+int cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  if (g_cu_count[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_cu_count[dev] = n;
+  }
+  return g_cu_count[dev];
+}
+
+unsigned grid_for(size_t work_items_per_block_units) {
+  size_t g = work_items_per_block_units ? work_items_per_block_units : 1;
+  if (g_blocks_per_cu > 0) {
+    size_t cap = (size_t)cu_count() * (size_t)g_blocks_per_cu;
+    if (g > cap) g = cap;
+  }
+  if (g > 0x7fffffffu) g = 0x7fffffffu;
+  return (unsigned)g;
+}
+
+struct Plan {
+  bool vec;
+  unsigned head, tail;
+  size_t nvec;
+  unsigned grid;
+};
+
+Plan plan_for(const void* out, const void* a, const void* b, size_t n, size_t es) {
+  Plan p{};
+  const size_t W = 16 / es;
+  uintptr_t mo = (uintptr_t)out & 15, ma = (uintptr_t)a & 15, mb = (uintptr_t)b & 15;
+  if (mo == ma && mo == mb && (mo % es) == 0) {
+    size_t head = mo ? (16 - mo) / es : 0;
+    if (head > n) head = n;
+    size_t rest = n - head;
+    p.vec = true;
+    p.head = (unsigned)head;
+    p.nvec = rest / W;
+    p.tail = (unsigned)(rest % W);
+    size_t tiles = (p.nvec + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+    p.grid = grid_for(tiles);
+  } else {
+    p.vec = false;
+    p.grid = grid_for((n + kBlock - 1) / kBlock);
+  }
+  return p;
+}
+
+template <typename T, int OP>
+hipError_t launch_t(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
+  Plan p = plan_for(out, a, b, n, sizeof(T));
+  if (p.vec) {
+    if (g_nontemporal)
+      hipLaunchKernelGGL((k_reduce_vec<T, OP, true>), dim3(p.grid), dim3(kBlock), 0, s,
+                         out, a, b, p.head, p.nvec, p.tail);
+    else
+      hipLaunchKernelGGL((k_reduce_vec<T, OP, false>), dim3(p.grid), dim3(kBlock), 0, s,
+                         out, a, b, p.head, p.nvec, p.tail);
+  } else {
+    hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(p.grid), dim3(kBlock), 0, s, out, a, b, n);
+  }
+  return hipGetLastError();
+}
+
+int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, void* stream) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
+  if (n == 0) return 0;
+  if (!out || !a || !b) { set_err("pgk: NULL buffer with n=%zu", n); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (dt == PGK_DT_INT32) {
+    uint32_t* o = (uint32_t*)out;
+    const uint32_t* x = (const uint32_t*)a;
+    const uint32_t* y = (const uint32_t*)b;
+    e = op == PGK_OP_SUM ? launch_t<uint32_t, PGK_OP_SUM>(o, x, y, n, s)
+                         : launch_t<uint32_t, PGK_OP_PROD>(o, x, y, n, s);
+  } else {
+    double* o = (double*)out;
+    const double* x = (const double*)a;
+    const double* y = (const double*)b;
+    e = op == PGK_OP_SUM ? launch_t<double, PGK_OP_SUM>(o, x, y, n, s)
+                         : launch_t<double, PGK_OP_PROD>(o, x, y, n, s);
+  }
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pgk_reduce(void* dst, const void* src, size_t n, int dt, int op, void* stream) {
+  return launch(dst, dst, src, n, dt, op, stream);
+}
+
+int pgk_reduce_out(void* out, const void* a, const void* b, size_t n, int dt, int op,
+                   void* stream) {
+  return launch(out, a, b, n, dt, op, stream);
+}
+
+int pgk_device_count(int* count) {
+  if (!count) { set_err("pgk: NULL count"); return -1; }
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) { *count = 0; set_err("pgk: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_set_device(int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { set_err("pgk: hipSetDevice(%d): %s", device, hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_synchronize(void) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) { set_err("pgk: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_tune(int blocks_per_cu, int nontemporal) {
+  if (blocks_per_cu >= 0) g_blocks_per_cu = blocks_per_cu;
+  if (nontemporal >= 0) g_nontemporal = nontemporal ? 1 : 0;
+  return 0;
+}
+
+int pgk_launch_geometry(size_t n, int dt, unsigned* grid, unsigned* block) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  Plan p = plan_for(nullptr, nullptr, nullptr, n, dt == PGK_DT_INT32 ? 4 : 8);
+  if (grid) *grid = p.grid;
+  if (block) *block = kBlock;
+  return 0;
+}
+
+const char* pgk_last_error(void) { return g_err; }
+
+#define PGK_STR2(x) #x
+#define PGK_STR(x) PGK_STR2(x)
+const char* pgk_version(void) {
+  return "pgk gfx950 (HIP " PGK_STR(HIP_VERSION_MAJOR) "." PGK_STR(HIP_VERSION_MINOR) ")";
+}
+
+}  // extern "C"

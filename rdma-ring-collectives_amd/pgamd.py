@@ -1,0 +1,185 @@
+"""ctypes binding of libpg_amd.so (include/pg.h, include/pg_ext.h, include/pgk.h).
+
+This is how Python callers (tests, bench.py, __graft_entry__) reach the C-ABI;
+a C/C++ caller links libpg_amd.so directly.  There is no Python or CPU
+implementation of any collective or reduction here: if the shared library is
+missing, `load()` raises.
+
+PyTorch, when present, is imported before the library is opened so that both
+resolve the same HIP runtime (libamdhip64.so.7 is matched by SONAME).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libpg_amd.so"
+REPO_ROOT = PKG_DIR.parent
+
+# include/pg.h (reference pg.h:78-87)
+DT_INT32, DT_DOUBLE = 0, 1
+OP_SUM, OP_PROD = 0, 1
+# include/pg_ext.h
+PG_TRANSPORT_RCCL, PG_TRANSPORT_LOOPBACK, PG_TRANSPORT_THREADS, PG_TRANSPORT_SELF = 0, 1, 2, 3
+PG_BUF_NONE, PG_BUF_SRC, PG_BUF_OUT, PG_BUF_STAGE0, PG_BUF_STAGE1 = 0, 1, 2, 3, 4
+PG_COLL_REDUCE_SCATTER, PG_COLL_ALL_GATHER, PG_COLL_ALL_REDUCE = 0, 1, 2
+
+ELEM_SIZE = {DT_INT32: 4, DT_DOUBLE: 8}
+
+
+class PgStep(ctypes.Structure):
+    """struct pg_step (include/pg_ext.h)."""
+    _fields_ = [
+        ("round", ctypes.c_int32), ("batch", ctypes.c_int32), ("seg", ctypes.c_int32),
+        ("send_wait", ctypes.c_int32),
+        ("send_buf", ctypes.c_int32), ("recv_buf", ctypes.c_int32),
+        ("red_dst_buf", ctypes.c_int32), ("red_src_buf", ctypes.c_int32),
+        ("send_off", ctypes.c_int64), ("send_bytes", ctypes.c_int64),
+        ("recv_off", ctypes.c_int64), ("recv_bytes", ctypes.c_int64),
+        ("red_dst_off", ctypes.c_int64), ("red_src_off", ctypes.c_int64),
+        ("red_elems", ctypes.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class PgStats(ctypes.Structure):
+    """struct pg_stats (include/pg_ext.h)."""
+    _fields_ = [
+        ("wall_us", ctypes.c_double), ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double),
+        ("ring_us", ctypes.c_double),
+        ("reduce_launches", ctypes.c_int64), ("reduce_elems", ctypes.c_int64),
+        ("bytes_sent", ctypes.c_int64), ("bytes_recv", ctypes.c_int64),
+    ]
+
+
+class PgHead(ctypes.Structure):
+    """Leading fields of struct pg (include/pg.h) -- what a reference harness reads/sets."""
+    _fields_ = [
+        ("rank", ctypes.c_int), ("world_size", ctypes.c_int),
+        ("chunk_bytes", ctypes.c_size_t), ("eager_max", ctypes.c_size_t),
+        ("inflight", ctypes.c_int),
+        ("hosts", ctypes.POINTER(ctypes.c_char_p)), ("port", ctypes.c_int),
+        ("device", ctypes.c_int), ("transport", ctypes.c_int), ("impl", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+_VP, _CVP, _SZ, _I = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+_SIGS = {
+    # include/pg.h
+    "connect_process_group": (_I, [ctypes.c_char_p, ctypes.POINTER(_VP)]),
+    "pg_close": (_I, [_VP]),
+    "pg_all_reduce": (_I, [_VP, _VP, _I, _I, _I, _VP]),
+    "pg_reduce_scatter": (_I, [_VP, _VP, _I, _I, _I, _VP]),
+    "pg_all_gather": (_I, [_VP, _VP, _I, _I, _VP]),
+    # include/pg_ext.h
+    "pg_block_range": (_I, [_I, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "pg_plan_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _SZ, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_connect_local": (_I, [_I, _I, _I, ctypes.POINTER(_VP)]),
+    "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I]),
+    "pg_get_stats": (_I, [_VP, ctypes.POINTER(PgStats)]),
+    "pg_last_error": (ctypes.c_char_p, []),
+    # include/pgk.h
+    "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
+    "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
+    "pgk_device_count": (_I, [ctypes.POINTER(_I)]),
+    "pgk_set_device": (_I, [_I]),
+    "pgk_synchronize": (_I, []),
+    "pgk_tune": (_I, [_I, _I]),
+    "pgk_launch_geometry": (_I, [_SZ, _I, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
+    "pgk_last_error": (ctypes.c_char_p, []),
+    "pgk_version": (ctypes.c_char_p, []),
+}
+
+
+def load() -> ctypes.CDLL:
+    """Open libpg_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `make -C rdma-ring-collectives_amd` "
+            "or __graft_entry__.build(); there is no fallback implementation")
+    try:  # share torch's HIP runtime if torch is used in this process
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    lib = load()
+    msg = lib.pg_last_error() or b""
+    kmsg = lib.pgk_last_error() or b""
+    return (msg or kmsg).decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+
+
+def block_range(count: int, world: int, block: int) -> tuple[int, int]:
+    lib = load()
+    off, ln = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib.pg_block_range(count, world, block, ctypes.byref(off), ctypes.byref(ln)), "pg_block_range")
+    return off.value, ln.value
+
+
+def plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max=4096, inflight=4, alias=0):
+    lib = load()
+    n = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, alias, None, 0)
+    if n < 0:
+        raise ValueError("pg_plan_reduce_scatter: bad arguments")
+    arr = (PgStep * max(n, 1))()
+    m = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, alias, arr, n)
+    assert m == n
+    return [arr[i].as_dict() for i in range(n)]
+
+
+def plan_all_gather(rank, world, count, dt, uniform=1):
+    lib = load()
+    n = lib.pg_plan_all_gather(rank, world, count, dt, uniform, None, 0)
+    if n < 0:
+        raise ValueError("pg_plan_all_gather: bad arguments")
+    arr = (PgStep * max(n, 1))()
+    lib.pg_plan_all_gather(rank, world, count, dt, uniform, arr, n)
+    return [arr[i].as_dict() for i in range(n)]
+
+
+def head(handle) -> PgHead:
+    """View the public leading fields of a struct pg handle."""
+    return PgHead.from_address(handle if isinstance(handle, int) else handle.value)
+
+
+def stats(handle) -> dict:
+    lib = load()
+    st = PgStats()
+    check(lib.pg_get_stats(handle, ctypes.byref(st)), "pg_get_stats")
+    return {name: getattr(st, name) for name, _ in PgStats._fields_}
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/*.h (for the ABI export test)."""
+    import re
+    names = []
+    for h in sorted((REPO_ROOT / "include").glob("*.h")):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", text, flags=re.M):
+            name = m.group(1)
+            if name not in ("if", "for", "while", "return", "sizeof") and not name.isupper():
+                names.append(name)
+    return sorted(set(names))

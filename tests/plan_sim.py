@@ -1,0 +1,132 @@
+"""Test-side executor of libpg_amd.so's ring plans (struct pg_step), in numpy.
+
+Used to check the HOST SCHEDULE without a GPU: each rank's plan -- produced by
+the library's pg_plan_* C functions -- is executed with per-edge FIFO channels
+(the semantics of ncclSend/ncclRecv between ring neighbours) and the reduction
+is done here with numpy's wrapping/IEEE arithmetic.  This file is test
+infrastructure; nothing in the library calls it.
+"""
+from __future__ import annotations
+
+from collections import deque
+
+import numpy as np
+
+import pgamd
+
+NP = {0: np.int32, 1: np.float64}
+
+
+def np_reduce(dst: np.ndarray, src: np.ndarray, op: int) -> None:
+    if dst.dtype == np.int32:
+        d, s = dst.view(np.uint32), src.view(np.uint32)
+        if op == 0:
+            np.add(d, s, out=d)
+        else:
+            np.multiply(d, s, out=d)
+    else:
+        if op == 0:
+            np.add(dst, src, out=dst)
+        else:
+            np.multiply(dst, src, out=dst)
+
+
+def _view(bufs, which, off, nbytes):
+    b = bufs[which]
+    return b[off:off + nbytes]
+
+
+def run_plans(plans, bufs_per_rank, dt, op):
+    """Execute every rank's step list.  bufs_per_rank[r][PG_BUF_*] = uint8 arrays.
+    A step runs once all its receives are available; sends snapshot the bytes
+    at send time (a rank's steps run in order, so a forwarded partial is
+    already reduced, as the executor's red_ev wait guarantees)."""
+    world = len(plans)
+    chans = [deque() for _ in range(world)]     # chans[r]: r -> r+1
+    pos = [0] * world
+    # group steps into batches per rank
+    batches = []
+    for st in plans:
+        bl, cur = [], None
+        for s in st:
+            if cur is None or s["batch"] != cur[0]["batch"]:
+                cur = []
+                bl.append(cur)
+            cur.append(s)
+        batches.append(bl)
+    es = 4 if dt == 0 else 8
+    pending = [None] * world      # sends of a batch are posted before its receives
+    progress = True
+    while progress:
+        progress = False
+        for r in range(world):
+            if pos[r] >= len(batches[r]):
+                continue
+            batch = batches[r][pos[r]]
+            bufs = bufs_per_rank[r]
+            if pending[r] is None:
+                for s in batch:
+                    if s["send_bytes"]:
+                        chans[r].append(_view(bufs, s["send_buf"], s["send_off"], s["send_bytes"]).copy())
+                pending[r] = True
+                progress = True
+            left = chans[(r - 1) % world]
+            need = sum(1 for s in batch if s["recv_bytes"])
+            if len(left) < need:
+                continue
+            for s in batch:
+                if s["recv_bytes"]:
+                    msg = left.popleft()
+                    assert msg.size == s["recv_bytes"], (r, s, msg.size)
+                    _view(bufs, s["recv_buf"], s["recv_off"], s["recv_bytes"])[:] = msg
+            for s in batch:
+                if s["red_elems"]:
+                    d = _view(bufs, s["red_dst_buf"], s["red_dst_off"], s["red_elems"] * es).view(NP[dt])
+                    src = _view(bufs, s["red_src_buf"], s["red_src_off"], s["red_elems"] * es).view(NP[dt])
+                    np_reduce(d, src, op)
+            pos[r] += 1
+            pending[r] = None
+            progress = True
+    assert all(pos[r] == len(batches[r]) for r in range(world)), "deadlock"
+    assert all(len(c) == 0 for c in chans), "unconsumed messages"
+
+
+def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False):
+    world, count = len(sends), sends[0].size
+    es = 4 if dt == 0 else 8
+    bmax = -(-count // world) * es if count else 0
+    plans, bufs = [], []
+    for r in range(world):
+        plans.append(pgamd.plan_reduce_scatter(r, world, count, dt, chunk_bytes, eager_max, inflight, int(alias)))
+        off, ln = pgamd.block_range(count, world, r)
+        src = sends[r].copy().view(np.uint8)
+        if alias:
+            out = src[off * es:(off + ln) * es]
+        else:
+            out = np.zeros(ln * es, np.uint8)
+        bufs.append({pgamd.PG_BUF_SRC: src, pgamd.PG_BUF_OUT: out,
+                     pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)})
+    run_plans(plans, bufs, dt, op)
+    return [bufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)], bufs
+
+
+def ring_all_gather(sends, dt):
+    world, count = len(sends), sends[0].size
+    es = 4 if dt == 0 else 8
+    plans, bufs = [], []
+    for r in range(world):
+        plans.append(pgamd.plan_all_gather(r, world, count, dt, 1))
+        full = np.zeros(count * world * es, np.uint8)
+        full[r * count * es:(r + 1) * count * es] = sends[r].view(np.uint8)
+        bufs.append({pgamd.PG_BUF_OUT: full})
+    run_plans(plans, bufs, dt, 0)
+    return [b[pgamd.PG_BUF_OUT].view(NP[dt]).copy() for b in bufs]
+
+
+def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4):
+    world, count = len(sends), sends[0].size
+    _, bufs = ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max, inflight, alias=True)
+    plans = [pgamd.plan_all_gather(r, world, count, dt, 0) for r in range(world)]
+    agbufs = [{pgamd.PG_BUF_OUT: bufs[r][pgamd.PG_BUF_SRC]} for r in range(world)]
+    run_plans(plans, agbufs, dt, 0)
+    return [agbufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)]

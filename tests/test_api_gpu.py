@@ -1,0 +1,261 @@
+"""include/pg.h collectives on the GPU.
+
+  * world_size == 1 and the LOOPBACK transport reproduce the reference's own
+    outputs (tests/golden/, from the compiled src/pg.c) -- including its mock
+    reduce-scatter schedule at W = 2..8 and its summing mock all-gather.
+  * the ring (W virtual ranks in one process: PG_TRANSPORT_THREADS, same plan,
+    executor, streams, events and kernel as the RCCL path) equals the oracle's
+    ring simulator bit for bit, with device-resident and host buffers.
+"""
+import ctypes
+import itertools
+import socket
+
+import numpy as np
+import pytest
+
+import pgamd
+from gpu_util import open_local, ptr, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+NP = {0: np.int32, 1: np.float64}
+
+
+def both_memories(torch, a):
+    """(device tensor, host numpy) views of the same initial data."""
+    return to_dev(torch, a), np.array(a, copy=True)
+
+
+def test_world1_api(gpu, lib, golden):
+    torch = gpu
+    man, arr = golden
+    h = open_local(lib, 0, 1, pgamd.PG_TRANSPORT_SELF)
+    try:
+        for c in man["w1"]:
+            k, dt, op, n = c["key"], c["dt"], c["op"], c["count"]
+            send, recv0 = arr[k + "_send"], arr[k + "_recv0"]
+            for on_dev in (True, False):
+                S = to_dev(torch, send) if on_dev else send.copy()
+                for fn, want in (("rs", arr[k + "_rs"]), ("ag", arr[k + "_ag"]), ("ar", arr[k + "_ar"])):
+                    R = to_dev(torch, recv0) if on_dev else recv0.copy()
+                    sp = ptr(S) if on_dev else S.ctypes.data
+                    rp = ptr(R) if on_dev else R.ctypes.data
+                    if fn == "rs":
+                        rc = lib.pg_reduce_scatter(sp, rp, n, dt, op, h)
+                    elif fn == "ag":
+                        rc = lib.pg_all_gather(sp, rp, n, dt, h)
+                    else:
+                        rc = lib.pg_all_reduce(sp, rp, n, dt, op, h)
+                    assert rc == 0, pgamd.last_error()
+                    got = to_host(torch, R) if on_dev else R
+                    assert got.tobytes() == want.tobytes(), (k, fn, on_dev)
+                # in-place all-reduce
+                B = to_dev(torch, send) if on_dev else send.copy()
+                bp = ptr(B) if on_dev else B.ctypes.data
+                assert lib.pg_all_reduce(bp, bp, n, dt, op, h) == 0
+                assert (to_host(torch, B) if on_dev else B).tobytes() == arr[k + "_arip"].tobytes()
+    finally:
+        lib.pg_close(h)
+
+
+def test_connect_process_group_single_host(gpu, lib, monkeypatch):
+    torch = gpu
+    for var in ("PG_RANK", "RANK", "PG_DEVICE", "LOCAL_RANK", "PG_TRANSPORT"):
+        monkeypatch.delenv(var, raising=False)
+    h = ctypes.c_void_p()
+    assert lib.connect_process_group(socket.gethostname().encode(), ctypes.byref(h)) == 0, pgamd.last_error()
+    hd = pgamd.head(h)
+    assert (hd.rank, hd.world_size, hd.transport) == (0, 1, pgamd.PG_TRANSPORT_SELF)
+    x = np.arange(10, dtype=np.float64)
+    X = to_dev(torch, x)
+    Y = to_dev(torch, np.zeros(10))
+    assert lib.pg_all_reduce(ptr(X), ptr(Y), 10, 1, 0, h) == 0
+    assert to_host(torch, Y).tobytes() == x.tobytes()
+    assert lib.pg_close(h) == 0
+    # env precedence: PG_CHUNK_BYTES wins over the default (reference bug)
+    monkeypatch.setenv("PG_CHUNK_BYTES", "65536")
+    monkeypatch.setenv("PG_INFLIGHT", "7")
+    assert lib.connect_process_group(socket.gethostname().encode(), ctypes.byref(h)) == 0
+    assert (pgamd.head(h).chunk_bytes, pgamd.head(h).inflight) == (65536, 7)
+    lib.pg_close(h)
+    assert lib.connect_process_group(b"host-that-is-not-me", ctypes.byref(h)) == -1
+
+
+def test_error_codes_match_reference(gpu, lib, golden):
+    torch = gpu
+    man, _ = golden
+    t = torch.zeros(16, dtype=torch.int32, device="cuda")
+    p = ptr(t)
+    h1 = open_local(lib, 0, 1, pgamd.PG_TRANSPORT_SELF)
+    h2 = open_local(lib, 0, 2, pgamd.PG_TRANSPORT_LOOPBACK)
+    try:
+        got = {
+            ("reduce_scatter", "null_send"): lib.pg_reduce_scatter(None, p, 8, 0, 0, h2),
+            ("reduce_scatter", "null_recv"): lib.pg_reduce_scatter(p, None, 8, 0, 0, h2),
+            ("reduce_scatter", "negative_count"): lib.pg_reduce_scatter(p, p, -1, 0, 0, h2),
+            ("reduce_scatter", "bad_datatype"): lib.pg_reduce_scatter(p, p, 8, 7, 0, h2),
+            ("reduce_scatter", "zero_count"): lib.pg_reduce_scatter(p, p, 0, 0, 0, h2),
+            ("all_gather", "null_recv"): lib.pg_all_gather(p, None, 8, 0, h2),
+            ("all_gather", "negative_count"): lib.pg_all_gather(p, p, -1, 0, h2),
+            ("all_gather", "bad_datatype"): lib.pg_all_gather(p, p, 8, 7, h2),
+            ("all_gather", "null_send_world1"): lib.pg_all_gather(None, p, 8, 0, h1),
+            ("all_reduce", "null_send"): lib.pg_all_reduce(None, p, 8, 0, 0, h1),
+            ("all_reduce", "null_recv"): lib.pg_all_reduce(p, None, 8, 0, 0, h1),
+            ("all_reduce", "negative_count"): lib.pg_all_reduce(p, p, -1, 0, 0, h1),
+            ("all_reduce", "bad_datatype"): lib.pg_all_reduce(p, p, 8, 7, 0, h1),
+        }
+        for e in man["errors"]:
+            assert got[(e["fn"], e["case"])] == e["rc"], e
+    finally:
+        lib.pg_close(h1)
+        lib.pg_close(h2)
+
+
+def test_loopback_mock_reduce_scatter(gpu, lib, golden):
+    """The reference's mock schedule (src/pg.c:264-291) at W = 2,3,4,8, every
+    rank, run on the GPU kernel: identical to the reference's outputs."""
+    torch = gpu
+    man, arr = golden
+    handles = {}
+    try:
+        for i, c in enumerate(man["mock_rs"]):
+            key = (c["rank"], c["world"])
+            if key not in handles:
+                handles[key] = open_local(lib, c["rank"], c["world"], pgamd.PG_TRANSPORT_LOOPBACK)
+            h = handles[key]
+            pgamd.head(h).chunk_bytes = c["chunk_bytes"]       # as a reference harness would
+            k, dt, op, n = c["key"], c["dt"], c["op"], c["count"]
+            on_dev = i % 2 == 0
+            if c.get("in_place"):
+                B = to_dev(torch, arr[k + "_buf0"]) if on_dev else arr[k + "_buf0"].copy()
+                bp = ptr(B) if on_dev else B.ctypes.data
+                assert lib.pg_reduce_scatter(bp, bp, n, dt, op, h) == 0, pgamd.last_error()
+                got = to_host(torch, B) if on_dev else B
+                assert got.tobytes() == arr[k + "_buf1"].tobytes(), c
+                continue
+            S = to_dev(torch, arr[k + "_send"]) if on_dev else arr[k + "_send"].copy()
+            R = to_dev(torch, arr[k + "_recv0"]) if on_dev else arr[k + "_recv0"].copy()
+            sp, rp = (ptr(S), ptr(R)) if on_dev else (S.ctypes.data, R.ctypes.data)
+            assert lib.pg_reduce_scatter(sp, rp, n, dt, op, h) == 0, pgamd.last_error()
+            got = to_host(torch, R) if on_dev else R
+            assert got.tobytes() == arr[k + "_recv1"].tobytes(), c
+    finally:
+        for h in handles.values():
+            lib.pg_close(h)
+
+
+def test_loopback_mock_all_gather_and_refusals(gpu, lib, golden):
+    torch = gpu
+    man, arr = golden
+    handles = {}
+    try:
+        for i, c in enumerate(man["mock_ag"]):
+            key = (c["rank"], c["world"])
+            if key not in handles:
+                handles[key] = open_local(lib, c["rank"], c["world"], pgamd.PG_TRANSPORT_LOOPBACK)
+            h, k, dt, n = handles[key], c["key"], c["dt"], c["count"]
+            on_dev = i % 2 == 1
+            R = to_dev(torch, arr[k + "_recv0"]) if on_dev else arr[k + "_recv0"].copy()
+            rp = ptr(R) if on_dev else R.ctypes.data
+            sp = None
+            if c["with_send"]:
+                S = to_dev(torch, arr[k + "_send"]) if on_dev else arr[k + "_send"].copy()
+                sp = ptr(S) if on_dev else S.ctypes.data
+            assert lib.pg_all_gather(sp, rp, n, dt, h) == 0, pgamd.last_error()
+            got = to_host(torch, R) if on_dev else R
+            assert got.tobytes() == arr[k + "_recv1"].tobytes(), c
+        # W > 1 all-reduce and out-of-bounds reduce-scatter shapes are refused, not run
+        h = open_local(lib, 1, 2, pgamd.PG_TRANSPORT_LOOPBACK)
+        handles[(1, 2, "x")] = h
+        t = torch.zeros(64, dtype=torch.int32, device="cuda")
+        assert lib.pg_all_reduce(ptr(t), ptr(t), 64, 0, 0, h) == -1
+        pgamd.head(h).chunk_bytes = 16                      # 4 elements per chunk
+        assert lib.pg_reduce_scatter(ptr(t), ptr(t), 6, 0, 0, h) == -1   # send chunk 1 of 6 is short
+        assert "past sendbuf" in pgamd.last_error()
+    finally:
+        for h in handles.values():
+            lib.pg_close(h)
+
+
+def sim(lib, torch, coll, sends, recvs, count, dt, op, chunk_bytes, eager_max, inflight, on_dev):
+    world = len(sends)
+    if on_dev:
+        S = [to_dev(torch, s) for s in sends]
+        R = [to_dev(torch, r) for r in recvs]
+        sp = (ctypes.c_void_p * world)(*[ptr(s) for s in S])
+        rp = (ctypes.c_void_p * world)(*[ptr(r) for r in R])
+    else:
+        S = [s.copy() for s in sends]
+        R = [r.copy() for r in recvs]
+        sp = (ctypes.c_void_p * world)(*[s.ctypes.data for s in S])
+        rp = (ctypes.c_void_p * world)(*[r.ctypes.data for r in R])
+    rc = lib.pgx_sim_run(world, coll, sp, rp, count, dt, op, chunk_bytes, eager_max, inflight)
+    assert rc == 0, pgamd.last_error()
+    return [to_host(torch, r) if on_dev else r for r in R]
+
+
+CASES = [  # world, dt, op, count, chunk_bytes, eager_max, inflight
+    (2, 0, 0, 1, 64, 0, 1), (2, 1, 1, 1000, 64, 0, 3), (2, 1, 0, 1 << 16, 1 << 20, 4096, 4),
+    (3, 0, 1, 7, 8, 0, 1), (3, 1, 0, 4099, 1024, 0, 2), (3, 0, 0, 0, 64, 0, 1),
+    (4, 1, 0, 100003, 1 << 16, 4096, 4), (4, 0, 1, 4096, 4096, 4096, 1), (4, 1, 1, 5, 8, 0, 2),
+    (8, 1, 0, 65536 + 3, 1 << 14, 0, 4), (8, 0, 0, 8, 4, 0, 1), (8, 1, 1, 1001, 128, 0, 8),
+    (5, 1, 0, 12345, 2048, 4096, 2),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_ring_reduce_scatter_sim(gpu, lib, oracle, case):
+    world, dt, op, count, cb, eager, infl = case
+    xs = [oracle.fill(count, dt, op, 1000 + 7 * r + count) for r in range(world)]
+    want = oracle.ring_reduce_scatter(xs, dt, op)
+    for on_dev in (True, False):
+        recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want]
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, cb, eager, infl, on_dev)
+        for r in range(world):
+            assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (case, r, on_dev)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_ring_all_reduce_sim(gpu, lib, oracle, case):
+    world, dt, op, count, cb, eager, infl = case
+    xs = [oracle.fill(count, dt, op, 2000 + 3 * r + count) for r in range(world)]
+    want = oracle.ring_all_reduce(xs, dt, op)
+    for on_dev, in_place in itertools.product((True, False), (False, True)):
+        recvs = [x.copy() if in_place else np.zeros(count, NP[dt]) for x in xs]
+        if in_place:
+            torch = gpu
+            R = [to_dev(torch, r) for r in recvs] if on_dev else recvs
+            ps = (ctypes.c_void_p * world)(*[(ptr(r) if on_dev else r.ctypes.data) for r in R])
+            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, cb, eager, infl) == 0, \
+                pgamd.last_error()
+            got = [to_host(torch, r) if on_dev else r for r in R]
+        else:
+            got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, recvs, count, dt, op, cb, eager, infl, on_dev)
+        for r in range(world):
+            assert got[r].tobytes() == want[r].tobytes(), (case, r, on_dev, in_place)
+
+
+@pytest.mark.parametrize("world,count", [(2, 1), (3, 1000), (4, 0), (8, 4099)])
+def test_ring_all_gather_sim(gpu, lib, oracle, world, count):
+    for dt in (0, 1):
+        xs = [oracle.fill(count, dt, 0, 3000 + r) for r in range(world)]
+        want = oracle.ring_all_gather(xs, dt)
+        for on_dev in (True, False):
+            recvs = [np.zeros(count * world, NP[dt]) for _ in range(world)]
+            got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, recvs, count, dt, 0, 4096, 0, 1, on_dev)
+            for r in range(world):
+                assert got[r].tobytes() == want[r].tobytes()
+
+
+def test_ring_large_device_resident(gpu, lib, oracle):
+    """A 4-rank, 64 Mi-element double sum (512 MiB per rank) with 4 MiB
+    segments: bit-exact against the oracle."""
+    torch = gpu
+    world, count, dt, op = 4, 1 << 26, 1, 0
+    xs = [oracle.fill(count, dt, op, 4000 + r) for r in range(world)]
+    want = oracle.ring_reduce_scatter(xs, dt, op)
+    recvs = [np.zeros(w.size, np.float64) for w in want]
+    got = sim(lib, torch, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, 4 << 20, 4096, 4, True)
+    for r in range(world):
+        assert got[r].tobytes() == want[r].tobytes()
+    torch.cuda.empty_cache()

@@ -1,0 +1,126 @@
+"""gfx950 reduction kernel (include/pgk.h) against the reference's own outputs.
+
+Golden vectors come from the reference's compiled reduce_inplace
+(src/pg.c:151-159, tests/golden/); larger inputs are checked against the CPU
+oracle (a restatement pinned to the same vectors).  int32: bit-exact.  double:
+bit-exact for every non-NaN result; a NaN result must be NaN (tolerance stated
+in DESIGN.md: IEEE-754 leaves the NaN payload/sign of an invalid operation to
+the implementation; x86 SSE and CDNA produce different default NaNs)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from gpu_util import ptr, same_bits_nan_aware, stream, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def run(lib, torch, d0, s, dt, op):
+    d, sd = to_dev(torch, d0), to_dev(torch, s)
+    assert lib.pgk_reduce(ptr(d), ptr(sd), d0.size, dt, op, stream(torch)) == 0
+    return to_host(torch, d)
+
+
+def test_kernel_kats(gpu, lib, golden, oracle):
+    man, arr = golden
+    for c in man["kernel"]:
+        d0 = oracle.fill(c["n"], c["dt"], c["op"], c["seed_dst"])
+        s = oracle.fill(c["n"], c["dt"], c["op"], c["seed_src"])
+        assert sha(d0) == c["sha_dst0"]
+        out = run(lib, gpu, d0, s, c["dt"], c["op"])
+        assert sha(out) == c["sha_out"], c
+        if c["stored"]:
+            assert out.tobytes() == arr[c["key"] + "_out"].tobytes()
+
+
+def test_special_values(gpu, lib, golden):
+    man, arr = golden
+    for c in man["specials"]:
+        k = c["key"]
+        out = run(lib, gpu, arr[k + "_dst0"], arr[k + "_src"], c["dt"], c["op"])
+        assert same_bits_nan_aware(out, arr[k + "_out"]), k
+        if c["dt"] == 1:  # denormals must survive (no flush-to-zero)
+            want = arr[k + "_out"]
+            sub = (want != 0) & (np.abs(want) < np.finfo(np.float64).tiny)
+            assert sub.any() and np.array_equal(out[sub], want[sub])
+
+
+@pytest.mark.parametrize("dt", [0, 1])
+@pytest.mark.parametrize("op", [0, 1])
+def test_offsets_and_ragged_lengths(gpu, lib, oracle, dt, op):
+    """Head/tail peeling (pointers congruent mod 16 B) and the scalar path
+    (not congruent), for every small offset pair and ragged length."""
+    torch = gpu
+    base = 4096 + 9
+    d_all = oracle.fill(base + 8, dt, op, 11)
+    s_all = oracle.fill(base + 8, dt, op, 12)
+    D, S = to_dev(torch, d_all), to_dev(torch, s_all)
+    es = 4 if dt == 0 else 8
+    for od in range(4):
+        for os_ in range(4):
+            for n in (0, 1, 2, 3, 5, 17, 255, 1024, 4099):
+                D.copy_(torch.from_numpy(d_all))
+                assert lib.pgk_reduce(ptr(D) + od * es, ptr(S) + os_ * es, n, dt, op, stream(torch)) == 0
+                got = to_host(torch, D)
+                want = d_all.copy()
+                want[od:od + n] = oracle.reduce(d_all[od:od + n], s_all[os_:os_ + n], dt, op)
+                assert got.tobytes() == want.tobytes(), (od, os_, n)
+
+
+def test_reduce_out_and_aliasing(gpu, lib, oracle):
+    torch = gpu
+    for dt in (0, 1):
+        for op in (0, 1):
+            n = 100003
+            a, b = oracle.fill(n, dt, op, 5), oracle.fill(n, dt, op, 6)
+            want = oracle.reduce(a, b, dt, op)
+            A, B, O = to_dev(torch, a), to_dev(torch, b), to_dev(torch, np.zeros_like(a))
+            assert lib.pgk_reduce_out(ptr(O), ptr(A), ptr(B), n, dt, op, stream(torch)) == 0
+            assert to_host(torch, O).tobytes() == want.tobytes()
+            assert to_host(torch, A).tobytes() == a.tobytes()          # inputs untouched
+            assert lib.pgk_reduce_out(ptr(B), ptr(A), ptr(B), n, dt, op, stream(torch)) == 0   # out == b
+            assert to_host(torch, B).tobytes() == want.tobytes()
+    # dst == src: d = d op d
+    x = oracle.fill(4097, 1, 0, 9)
+    X = to_dev(torch, x)
+    assert lib.pgk_reduce(ptr(X), ptr(X), x.size, 1, 0, stream(torch)) == 0
+    assert to_host(torch, X).tobytes() == oracle.reduce(x, x, 1, 0).tobytes()
+
+
+@pytest.mark.parametrize("blocks_per_cu,nt", [(0, 0), (0, 1), (4, 0), (8, 1), (1, 1)])
+def test_tuning_variants_agree(gpu, lib, oracle, blocks_per_cu, nt):
+    torch = gpu
+    n = (1 << 20) + 3
+    try:
+        assert lib.pgk_tune(blocks_per_cu, nt) == 0
+        for dt in (0, 1):
+            a, b = oracle.fill(n, dt, 0, 21), oracle.fill(n, dt, 0, 22)
+            assert run(lib, torch, a, b, dt, 0).tobytes() == oracle.reduce(a, b, dt, 0).tobytes()
+    finally:
+        lib.pgk_tune(8, 1)
+
+
+def test_full_size_config2(gpu, lib, oracle):
+    """BASELINE config 2 size: 256 MiB double sum (and int32 prod at 256 MiB),
+    compared element-for-element with the oracle."""
+    torch = gpu
+    for dt, op, n in ((1, 0, 1 << 25), (0, 1, 1 << 26)):
+        a, b = oracle.fill(n, dt, op, 31), oracle.fill(n, dt, op, 32)
+        got = run(lib, torch, a, b, dt, op)
+        assert got.tobytes() == oracle.reduce(a, b, dt, op).tobytes()
+        del got
+        torch.cuda.empty_cache()
+
+
+def test_invalid_arguments(gpu, lib):
+    torch = gpu
+    t = torch.zeros(16, dtype=torch.int32, device="cuda")
+    assert lib.pgk_reduce(ptr(t), ptr(t), 16, 2, 0, stream(torch)) == -1
+    assert lib.pgk_reduce(ptr(t), ptr(t), 16, 0, 2, stream(torch)) == -1
+    assert lib.pgk_reduce(ptr(t), None, 16, 0, 0, stream(torch)) == -1
+    assert lib.pgk_reduce(ptr(t), ptr(t), 0, 0, 0, stream(torch)) == 0

@@ -1,0 +1,100 @@
+"""The N>1 path on CPU: world_size 2 and 4 over torch.distributed gloo.
+
+Each process asks libpg_amd.so for ITS rank's plan (pg_plan_reduce_scatter /
+pg_plan_all_gather, the schedule the GPU executor runs) and executes it with
+real point-to-point messages between processes; the segment reduction is done
+test-side with numpy.  Results must equal the oracle's ring simulator bit for
+bit.  This pins the multi-process schedule: every send pairs with the right
+neighbour's receive, in order, with matching sizes."""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd"), str(ROOT / "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pgamd
+        from oracle.pyoracle import Oracle
+        from plan_sim import NP, np_reduce
+        orc = Oracle()
+        right, left = (rank + 1) % world, (rank - 1) % world
+        fails = []
+        for dt, op, count, cb, infl in ((0, 0, 1000, 64, 2), (1, 0, 4099, 256, 4), (1, 1, 77, 8, 1),
+                                        (0, 1, 3, 4, 1), (1, 0, 0, 64, 1)):
+            es = 4 if dt == 0 else 8
+            xs = [orc.fill(count, dt, op, 500 + 17 * q_ + count) for q_ in range(world)]
+            want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+            off, ln = pgamd.block_range(count, world, rank)
+            bmax = -(-count // world) * es if count else 0
+            bufs = {pgamd.PG_BUF_SRC: xs[rank].copy().view(np.uint8), pgamd.PG_BUF_OUT: np.zeros(ln * es, np.uint8),
+                    pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)}
+            steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl)
+            i = 0
+            while i < len(steps):
+                j = i
+                while j < len(steps) and steps[j]["batch"] == steps[i]["batch"]:
+                    j += 1
+                reqs = []
+                for s in steps[i:j]:
+                    if s["send_bytes"]:
+                        t = torch.from_numpy(bufs[s["send_buf"]][s["send_off"]:s["send_off"] + s["send_bytes"]].copy())
+                        reqs.append(dist.isend(t, right))
+                    if s["recv_bytes"]:
+                        t = torch.empty(s["recv_bytes"], dtype=torch.uint8)
+                        reqs.append((dist.irecv(t, left), t, s))
+                for r_ in reqs:
+                    if isinstance(r_, tuple):
+                        r_[0].wait()
+                        s = r_[2]
+                        bufs[s["recv_buf"]][s["recv_off"]:s["recv_off"] + s["recv_bytes"]] = r_[1].numpy()
+                    else:
+                        r_.wait()
+                for s in steps[i:j]:
+                    if s["red_elems"]:
+                        n = s["red_elems"] * es
+                        d = bufs[s["red_dst_buf"]][s["red_dst_off"]:s["red_dst_off"] + n].view(NP[dt])
+                        src = bufs[s["red_src_buf"]][s["red_src_off"]:s["red_src_off"] + n].view(NP[dt])
+                        np_reduce(d, src, op)
+                i = j
+            got = bufs[pgamd.PG_BUF_OUT].view(NP[dt])
+            if got.tobytes() != want.tobytes():
+                fails.append((dt, op, count, cb))
+        q.put((rank, fails))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ring_plan_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, fails in results:
+        assert not fails, (rank, fails)
