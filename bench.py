@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
+    ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     return ap.parse_args()
 
 
@@ -109,26 +110,41 @@ def kernel_leg(lib, args, rank, world):
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
-    def step(i):
-        rc = lib.pgk_reduce(dst[i % N_PAIRS].data_ptr(), src[i % N_PAIRS].data_ptr(), N_ELEMS, DT, OP, sh)
+    # HIP events stamped by the kernel dispatch itself (hipExtLaunchKernelGGL
+    # start/stop, on the launch stream): per-launch kernel duration without
+    # separate marker packets in the stream
+    ev = []
+    for _ in range(args.steps):
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        pgamd.check(lib.pgk_event_create(ctypes.byref(a)), "event")
+        pgamd.check(lib.pgk_event_create(ctypes.byref(b)), "event")
+        ev.append((a, b))
+
+    def step(i, timed):
+        d, s = dst[i % N_PAIRS].data_ptr(), src[i % N_PAIRS].data_ptr()
+        rc = (lib.pgk_reduce_timed(d, s, N_ELEMS, DT, OP, sh, ev[i][0], ev[i][1]) if timed
+              else lib.pgk_reduce(d, s, N_ELEMS, DT, OP, sh))
         if rc != 0:
             raise RuntimeError(pgamd.last_error())
 
     for i in range(args.warmup):
-        step(i)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        step(i, False)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        step(i)
-        ev[i][1].record(stream)
+        step(i, True)
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
-    per_launch_ms = [a.elapsed_time(b) for a, b in ev]
+    per_launch_ms = []
+    for a, b in ev:
+        ms = ctypes.c_float()
+        pgamd.check(lib.pgk_event_elapsed_ms(a, b, ctypes.byref(ms)), "elapsed")
+        per_launch_ms.append(ms.value)
+        lib.pgk_event_destroy(a)
+        lib.pgk_event_destroy(b)
     del dst, src
     torch.cuda.empty_cache()
     return t1 - t0, per_launch_ms
@@ -168,6 +184,30 @@ def cpu_baseline(args):
             "sample": f"{reps} x reduce_inplace(double, sum) over 256 MiB chunks, {secs:.1f} s, "
                       f"1 pinned core of {os.cpu_count()} ({cpu}); "
                       f"{'oracle/_ref = reference src/pg.c:151-159 compiled -O2' if kind == 'reference' else 'oracle/pg_oracle.c restatement -O2'}"}
+
+
+def host_leg(lib, reps=3):
+    """PCIe-inclusive rate of the same chunk reduce with dst/src in host memory
+    (pgx_reduce_host: 64 MiB pieces, two streams).  Reported, never `value`."""
+    out = {}
+    n = N_ELEMS
+    for kind in ("pageable", "pinned"):
+        d = torch.rand(n, dtype=torch.float64)
+        s_ = torch.rand(n, dtype=torch.float64)
+        if kind == "pinned":
+            d, s_ = d.pin_memory(), s_.pin_memory()
+        pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 64 << 20), "host reduce")
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 64 << 20), "host reduce")
+        dt_ = (time.perf_counter() - t0) / reps
+        out[kind] = {"ms": round(dt_ * 1e3, 3), "traffic_gibs": round(3 * n * 8 / dt_ / GIB, 2),
+                     "payload_gibs": round(n * 8 / dt_ / GIB, 2),
+                     "pcie_gbs": round(3 * n * 8 / dt_ / 1e9, 2)}
+        del d, s_
+    out["note"] = ("256 MiB double sum, dst/src in host memory: H2D dst+src, reduce, D2H dst per "
+                   "64 MiB piece, 2 streams; pcie_gbs counts the 3*n*8 bytes that cross PCIe")
+    return out
 
 
 def load_traffic():
@@ -248,8 +288,14 @@ def main():
         except Exception as e:  # the primary measurement stands on its own
             ring = {"error": f"{type(e).__name__}: {e}"}
     cpu = None
+    host = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+    if world == 1 and not args.no_host:
+        try:
+            host = host_leg(lib)
+        except Exception as e:
+            host = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         traffic = load_traffic()
@@ -267,8 +313,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_mean_ms": round(mean_launch_ms, 5),
-                         "kernel_min_ms": round(float(np.min(per_launch_ms)), 5)},
+                         "kernel_min_ms": round(float(np.min(per_launch_ms)), 5),
+                         "timing": "per-launch hipExtLaunchKernelGGL start/stop events on the launch stream",
+                         "bytes_per_launch": bytes_per_step},
             "cpu_baseline": cpu,
+            "host_staged": host,
             "ring": ring,
             "kernel": pgamd.load().pgk_version().decode(),
         }

@@ -88,6 +88,12 @@ int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbuf
                 int count, int datatype, int op, size_t chunk_bytes,
                 size_t eager_max, int inflight);
 
+/* The hot path with both operands in host memory: dst[i] = dst[i] op src[i]
+ * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces on two
+ * streams (copies of one piece overlap the reduce of the previous one).
+ * Synchronous.  This is what the PCIe-inclusive rate in DESIGN.md measures. */
+int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
+
 /* Measurements of the last collective on this handle. */
 struct pg_stats {
   double wall_us;        /* host wall time of the call                      */

@@ -54,6 +54,20 @@ int pgk_synchronize(void);
  * (DESIGN.md). */
 int pgk_tune(int blocks_per_cu, int nontemporal);
 
+/* Vector-kernel shape: threads per block x 16-byte vectors per operand each
+ * thread keeps in flight.  Instantiated: 256x2, 256x4, 256x8, 512x2, 1024x1. */
+int pgk_tune_shape(int block, int unroll);
+
+/* pgk_reduce, with the kernel's own begin/end timestamps recorded into two
+ * HIP events (hipEvent_t as void*, from pgk_event_create) through
+ * hipExtLaunchKernelGGL: their elapsed time is the kernel's execution, without
+ * the dispatch overhead of separate event markers.  Used by bench.py. */
+int pgk_reduce_timed(void *dst, const void *src, size_t n, int dt, int op, void *stream,
+                     void *start_event, void *stop_event);
+int pgk_event_create(void **event);
+int pgk_event_destroy(void *event);
+int pgk_event_elapsed_ms(void *start_event, void *stop_event, float *ms);
+
 /* Grid the next pgk_reduce of n elements of dt would launch (for bench/tests). */
 int pgk_launch_geometry(size_t n, int dt, unsigned *grid, unsigned *block);
 

@@ -502,3 +502,51 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
   im->stats.wall_us = now_us() - t;
   return rc;
 }
+
+/* ---- host-memory reduce (the arriving-chunk step with host buffers) ------------ */
+
+/* dst[i] = dst[i] op src[i] with dst/src in host memory: chunked through HBM on
+ * two streams, so chunk k's copies overlap chunk k-1's reduce and write-back.
+ * Measures the PCIe-inclusive rate of the hot path (DESIGN.md §Host path). */
+int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes) {
+  size_t es = pg_elem_size(datatype);
+  if (!es || (op != PGK_OP_SUM && op != PGK_OP_PROD)) { pg_set_error("pgx_reduce_host: bad datatype/op"); return -1; }
+  if (!n) return 0;
+  if (!dst || !src) { pg_set_error("pgx_reduce_host: NULL buffer"); return -1; }
+  if (chunk_bytes < (1u << 20)) chunk_bytes = 64u << 20;
+  size_t ce = chunk_bytes / es;
+  hipStream_t st[2] = {NULL, NULL};
+  void *dd[2] = {NULL, NULL}, *ds[2] = {NULL, NULL};
+  int rc = -1;
+  for (int i = 0; i < 2; ++i) {
+    if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&dd[i], ce * es) != hipSuccess || hipMalloc(&ds[i], ce * es) != hipSuccess) {
+      pg_set_error("pgx_reduce_host: HIP allocation failed");
+      goto out;
+    }
+  }
+  for (size_t off = 0, k = 0; off < n; off += ce, ++k) {
+    size_t m = n - off < ce ? n - off : ce;
+    int s = (int)(k & 1);
+    char *hd = (char *)dst + off * es;
+    const char *hs = (const char *)src + off * es;
+    if (hipMemcpyAsync(dd[s], hd, m * es, hipMemcpyHostToDevice, st[s]) != hipSuccess ||
+        hipMemcpyAsync(ds[s], hs, m * es, hipMemcpyHostToDevice, st[s]) != hipSuccess) {
+      pg_set_error("pgx_reduce_host: H2D failed");
+      goto out;
+    }
+    if (pgk_reduce(dd[s], ds[s], m, datatype, op, (void *)st[s])) { pg_set_error("%s", pgk_last_error()); goto out; }
+    if (hipMemcpyAsync(hd, dd[s], m * es, hipMemcpyDeviceToHost, st[s]) != hipSuccess) {
+      pg_set_error("pgx_reduce_host: D2H failed");
+      goto out;
+    }
+  }
+  rc = 0;
+out:
+  for (int i = 0; i < 2; ++i) {
+    if (st[i]) { hipStreamSynchronize(st[i]); hipStreamDestroy(st[i]); }
+    if (dd[i]) hipFree(dd[i]);
+    if (ds[i]) hipFree(ds[i]);
+  }
+  return rc;
+}

@@ -16,6 +16,7 @@
 //             (built without -ffast-math / denormal flushing); no FMA is
 //             possible because each element sees exactly one operation.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdarg.h>
@@ -25,8 +26,11 @@
 
 namespace {
 
-constexpr int kBlock = 256;   // 4 waves of 64
-constexpr int kUnroll = 4;    // 16-B vectors per operand per thread per iteration
+// Vector kernel shape (threads per block kBlock, 16-B vectors per operand per
+// thread per iteration kUnroll) is a template; pgk_tune_shape picks one of the
+// instantiated pairs at run time.  Every pair moves 16 KiB per operand per
+// block iteration except 256x8 (32 KiB).
+constexpr int kScalarBlock = 256;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -57,7 +61,7 @@ __device__ __forceinline__ void st(X* p, X v) {
 // The vector region starts at element `head` and is 16-B aligned in all three
 // pointers; head/tail (< one vector each) are done by the first threads of
 // block 0.  Grid-strided so the host can cap the grid.
-template <typename T, int OP, bool NT>
+template <typename T, int OP, bool NT, int kBlock, int kUnroll>
 __global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
                                                        const T* __restrict__ a,
                                                        const T* __restrict__ b,
@@ -100,12 +104,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
 // segment starting at an odd element of an int32 buffer): element-wise, still
 // coalesced (lane i touches element i).
 template <typename T, int OP>
-__global__ __launch_bounds__(kBlock) void k_reduce_scalar(T* __restrict__ out,
-                                                          const T* __restrict__ a,
-                                                          const T* __restrict__ b,
-                                                          size_t n) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+__global__ __launch_bounds__(kScalarBlock) void k_reduce_scalar(T* __restrict__ out,
+                                                                const T* __restrict__ a,
+                                                                const T* __restrict__ b,
+                                                                size_t n) {
+  const size_t stride = (size_t)gridDim.x * kScalarBlock;
+  for (size_t i = (size_t)blockIdx.x * kScalarBlock + threadIdx.x; i < n; i += stride)
     out[i] = apply<OP>(a[i], b[i]);
 }
 
@@ -121,8 +125,10 @@ void set_err(const char* fmt, ...) {
 }
 
 // Tuning (process-wide).  Measured on MI355X: see DESIGN.md "Kernel tuning".
-int g_blocks_per_cu = 8;
+int g_blocks_per_cu = 0;   // one-shot grid: 6403 vs 6200 GB/s capped at 8/CU (sweep r01)
 int g_nontemporal = 1;
+int g_block = 1024;   // 1024x1: 6619 GB/s vs 6511 (256x4) at 256 MiB, sweep r01b
+int g_unroll = 1;
 
 constexpr int kMaxDevices = 64;
 int g_cu_count[kMaxDevices];  // 0 = not queried yet
@@ -168,32 +174,54 @@ Plan plan_for(const void* out, const void* a, const void* b, size_t n, size_t es
     p.head = (unsigned)head;
     p.nvec = rest / W;
     p.tail = (unsigned)(rest % W);
-    size_t tiles = (p.nvec + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+    size_t tile = (size_t)g_block * (size_t)g_unroll;
+    size_t tiles = (p.nvec + tile - 1) / tile;
     p.grid = grid_for(tiles);
   } else {
     p.vec = false;
-    p.grid = grid_for((n + kBlock - 1) / kBlock);
+    p.grid = grid_for((n + kScalarBlock - 1) / kScalarBlock);
   }
   return p;
 }
 
+// Every launch goes through hipExtLaunchKernelGGL so that a caller can ask for
+// the kernel's own begin/end timestamps (start/stop events; nullptr = none).
+struct Timing {
+  hipEvent_t start, stop;
+};
+
+template <typename T, int OP, bool NT, int B, int U>
+void launch_shape(const Plan& p, T* out, const T* a, const T* b, hipStream_t s, Timing tm) {
+  hipExtLaunchKernelGGL((k_reduce_vec<T, OP, NT, B, U>), dim3(p.grid), dim3(B), 0, s, tm.start, tm.stop, 0,
+                        out, a, b, p.head, p.nvec, p.tail);
+}
+
+template <typename T, int OP, bool NT>
+void launch_vec(const Plan& p, T* out, const T* a, const T* b, hipStream_t s, Timing tm) {
+  switch (g_block * 16 + g_unroll) {
+    case 256 * 16 + 2: launch_shape<T, OP, NT, 256, 2>(p, out, a, b, s, tm); break;
+    case 256 * 16 + 8: launch_shape<T, OP, NT, 256, 8>(p, out, a, b, s, tm); break;
+    case 512 * 16 + 2: launch_shape<T, OP, NT, 512, 2>(p, out, a, b, s, tm); break;
+    case 1024 * 16 + 1: launch_shape<T, OP, NT, 1024, 1>(p, out, a, b, s, tm); break;
+    default: launch_shape<T, OP, NT, 256, 4>(p, out, a, b, s, tm);
+  }
+}
+
 template <typename T, int OP>
-hipError_t launch_t(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
+hipError_t launch_t(T* out, const T* a, const T* b, size_t n, hipStream_t s, Timing tm) {
   Plan p = plan_for(out, a, b, n, sizeof(T));
   if (p.vec) {
-    if (g_nontemporal)
-      hipLaunchKernelGGL((k_reduce_vec<T, OP, true>), dim3(p.grid), dim3(kBlock), 0, s,
-                         out, a, b, p.head, p.nvec, p.tail);
-    else
-      hipLaunchKernelGGL((k_reduce_vec<T, OP, false>), dim3(p.grid), dim3(kBlock), 0, s,
-                         out, a, b, p.head, p.nvec, p.tail);
+    if (g_nontemporal) launch_vec<T, OP, true>(p, out, a, b, s, tm);
+    else launch_vec<T, OP, false>(p, out, a, b, s, tm);
   } else {
-    hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(p.grid), dim3(kBlock), 0, s, out, a, b, n);
+    hipExtLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(p.grid), dim3(kScalarBlock), 0, s, tm.start, tm.stop, 0,
+                          out, a, b, n);
   }
   return hipGetLastError();
 }
 
-int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, void* stream) {
+int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, void* stream,
+           Timing tm = Timing{nullptr, nullptr}) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (n == 0) return 0;
@@ -204,14 +232,14 @@ int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, vo
     uint32_t* o = (uint32_t*)out;
     const uint32_t* x = (const uint32_t*)a;
     const uint32_t* y = (const uint32_t*)b;
-    e = op == PGK_OP_SUM ? launch_t<uint32_t, PGK_OP_SUM>(o, x, y, n, s)
-                         : launch_t<uint32_t, PGK_OP_PROD>(o, x, y, n, s);
+    e = op == PGK_OP_SUM ? launch_t<uint32_t, PGK_OP_SUM>(o, x, y, n, s, tm)
+                         : launch_t<uint32_t, PGK_OP_PROD>(o, x, y, n, s, tm);
   } else {
     double* o = (double*)out;
     const double* x = (const double*)a;
     const double* y = (const double*)b;
-    e = op == PGK_OP_SUM ? launch_t<double, PGK_OP_SUM>(o, x, y, n, s)
-                         : launch_t<double, PGK_OP_PROD>(o, x, y, n, s);
+    e = op == PGK_OP_SUM ? launch_t<double, PGK_OP_SUM>(o, x, y, n, s, tm)
+                         : launch_t<double, PGK_OP_PROD>(o, x, y, n, s, tm);
   }
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
   return 0;
@@ -255,11 +283,43 @@ int pgk_tune(int blocks_per_cu, int nontemporal) {
   return 0;
 }
 
+int pgk_tune_shape(int block, int unroll) {
+  const int ok = (block == 256 && (unroll == 2 || unroll == 4 || unroll == 8)) ||
+                 (block == 512 && unroll == 2) || (block == 1024 && unroll == 1);
+  if (!ok) { set_err("pgk: shape %dx%d not instantiated", block, unroll); return -1; }
+  g_block = block;
+  g_unroll = unroll;
+  return 0;
+}
+
+int pgk_reduce_timed(void* dst, const void* src, size_t n, int dt, int op, void* stream,
+                     void* start_event, void* stop_event) {
+  return launch(dst, dst, src, n, dt, op, stream,
+                Timing{(hipEvent_t)start_event, (hipEvent_t)stop_event});
+}
+
+int pgk_event_create(void** ev) {
+  if (!ev) { set_err("pgk: NULL event slot"); return -1; }
+  hipError_t e = hipEventCreate((hipEvent_t*)ev);
+  if (e != hipSuccess) { set_err("pgk: hipEventCreate: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_event_destroy(void* ev) {
+  return ev && hipEventDestroy((hipEvent_t)ev) != hipSuccess ? -1 : 0;
+}
+
+int pgk_event_elapsed_ms(void* start, void* stop, float* ms) {
+  hipError_t e = hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
+  if (e != hipSuccess) { set_err("pgk: hipEventElapsedTime: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
 int pgk_launch_geometry(size_t n, int dt, unsigned* grid, unsigned* block) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   Plan p = plan_for(nullptr, nullptr, nullptr, n, dt == PGK_DT_INT32 ? 4 : 8);
   if (grid) *grid = p.grid;
-  if (block) *block = kBlock;
+  if (block) *block = p.vec ? (unsigned)g_block : (unsigned)kScalarBlock;
   return 0;
 }
 

@@ -84,6 +84,7 @@ _SIGS = {
     "pg_connect_local": (_I, [_I, _I, _I, ctypes.POINTER(_VP)]),
     "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I]),
     "pg_get_stats": (_I, [_VP, ctypes.POINTER(PgStats)]),
+    "pgx_reduce_host": (_I, [_VP, _CVP, _SZ, _I, _I, _SZ]),
     "pg_last_error": (ctypes.c_char_p, []),
     # include/pgk.h
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
@@ -92,6 +93,11 @@ _SIGS = {
     "pgk_set_device": (_I, [_I]),
     "pgk_synchronize": (_I, []),
     "pgk_tune": (_I, [_I, _I]),
+    "pgk_tune_shape": (_I, [_I, _I]),
+    "pgk_reduce_timed": (_I, [_VP, _CVP, _SZ, _I, _I, _VP, _VP, _VP]),
+    "pgk_event_create": (_I, [ctypes.POINTER(_VP)]),
+    "pgk_event_destroy": (_I, [_VP]),
+    "pgk_event_elapsed_ms": (_I, [_VP, _VP, ctypes.POINTER(ctypes.c_float)]),
     "pgk_launch_geometry": (_I, [_SZ, _I, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
     "pgk_last_error": (ctypes.c_char_p, []),
     "pgk_version": (ctypes.c_char_p, []),

@@ -8,12 +8,21 @@ import pgamd
 
 
 def to_dev(torch, a: np.ndarray):
+    """Device copy of `a`.  Zero-length arrays get a 1-element allocation so
+    the pointer is not NULL (a NULL buffer is an argument error, as in the
+    reference src/pg.c:267); the view keeps the zero length."""
+    if a.size == 0:
+        t = torch.zeros(1, dtype=torch.from_numpy(a[:0]).dtype, device="cuda")
+        t._logical_n = 0
+        return t
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
 def to_host(torch, t) -> np.ndarray:
     torch.cuda.synchronize()
-    return t.cpu().numpy()
+    out = t.cpu().numpy()
+    n = getattr(t, "_logical_n", None)
+    return out if n is None else out[:n]
 
 
 def ptr(t) -> int:

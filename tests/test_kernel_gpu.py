@@ -92,17 +92,38 @@ def test_reduce_out_and_aliasing(gpu, lib, oracle):
     assert to_host(torch, X).tobytes() == oracle.reduce(x, x, 1, 0).tobytes()
 
 
-@pytest.mark.parametrize("blocks_per_cu,nt", [(0, 0), (0, 1), (4, 0), (8, 1), (1, 1)])
-def test_tuning_variants_agree(gpu, lib, oracle, blocks_per_cu, nt):
+@pytest.mark.parametrize("blocks_per_cu,nt,shape", [(0, 0, (256, 4)), (0, 1, (512, 2)), (4, 0, (1024, 1)),
+                                                    (8, 1, (256, 8)), (1, 1, (256, 2)), (3, 1, (512, 2))])
+def test_tuning_variants_agree(gpu, lib, oracle, blocks_per_cu, nt, shape):
     torch = gpu
-    n = (1 << 20) + 3
     try:
         assert lib.pgk_tune(blocks_per_cu, nt) == 0
-        for dt in (0, 1):
-            a, b = oracle.fill(n, dt, 0, 21), oracle.fill(n, dt, 0, 22)
-            assert run(lib, torch, a, b, dt, 0).tobytes() == oracle.reduce(a, b, dt, 0).tobytes()
+        assert lib.pgk_tune_shape(*shape) == 0
+        for n in ((1 << 20) + 3, 4099, 77):
+            for dt in (0, 1):
+                a, b = oracle.fill(n, dt, 0, 21), oracle.fill(n, dt, 0, 22)
+                assert run(lib, torch, a, b, dt, 0).tobytes() == oracle.reduce(a, b, dt, 0).tobytes()
     finally:
-        lib.pgk_tune(8, 1)
+        lib.pgk_tune(0, 1)
+        lib.pgk_tune_shape(1024, 1)
+    assert lib.pgk_tune_shape(256, 3) == -1
+
+
+def test_timed_launch_events(gpu, lib, oracle):
+    import ctypes
+    torch = gpu
+    n = 1 << 22
+    a, b = oracle.fill(n, 1, 0, 41), oracle.fill(n, 1, 0, 42)
+    A, B = to_dev(torch, a), to_dev(torch, b)
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.pgk_event_create(ctypes.byref(e0)) == 0 and lib.pgk_event_create(ctypes.byref(e1)) == 0
+    assert lib.pgk_reduce_timed(ptr(A), ptr(B), n, 1, 0, stream(torch), e0, e1) == 0
+    torch.cuda.synchronize()
+    ms = ctypes.c_float()
+    assert lib.pgk_event_elapsed_ms(e0, e1, ctypes.byref(ms)) == 0 and 0 < ms.value < 100
+    assert to_host(torch, A).tobytes() == oracle.reduce(a, b, 1, 0).tobytes()
+    lib.pgk_event_destroy(e0)
+    lib.pgk_event_destroy(e1)
 
 
 def test_full_size_config2(gpu, lib, oracle):
@@ -124,3 +145,22 @@ def test_invalid_arguments(gpu, lib):
     assert lib.pgk_reduce(ptr(t), ptr(t), 16, 0, 2, stream(torch)) == -1
     assert lib.pgk_reduce(ptr(t), None, 16, 0, 0, stream(torch)) == -1
     assert lib.pgk_reduce(ptr(t), ptr(t), 0, 0, 0, stream(torch)) == 0
+
+
+def test_reduce_host_staged(gpu, lib, oracle):
+    """pgx_reduce_host: both operands in host memory (pageable and pinned),
+    chunked through HBM; identical to the oracle."""
+    torch = gpu
+    for dt, op, n, chunk in ((1, 0, (3 << 20) + 5, 1 << 20), (0, 1, 1000, 1 << 20), (1, 1, 1 << 22, 4 << 20)):
+        a, b = oracle.fill(n, dt, op, 51), oracle.fill(n, dt, op, 52)
+        want = oracle.reduce(a, b, dt, op)
+        d = a.copy()
+        assert lib.pgx_reduce_host(d.ctypes.data, b.ctypes.data, n, dt, op, chunk) == 0
+        assert d.tobytes() == want.tobytes()
+        pd = torch.from_numpy(a.copy()).pin_memory()
+        pb = torch.from_numpy(b).pin_memory()
+        assert lib.pgx_reduce_host(pd.data_ptr(), pb.data_ptr(), n, dt, op, chunk) == 0
+        assert pd.numpy().tobytes() == want.tobytes()
+    assert lib.pgx_reduce_host(None, None, 0, 1, 0, 0) == 0
+    assert lib.pgx_reduce_host(None, None, 5, 1, 0, 0) == -1
+    assert lib.pgx_reduce_host(None, None, 5, 3, 0, 0) == -1
