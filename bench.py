@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
+    ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
+    ap.add_argument("--transports", default="xgmi,rccl", help="ring-leg transports, comma separated")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     return ap.parse_args()
 
@@ -70,6 +72,9 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if os.environ.get("PG_BENCH_ONE_GPU") == "1":   # rehearsal of the N>1 path on a 1-GPU box
+        local = 0
+        os.environ["PG_DEVICE"] = "0"
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -222,8 +227,9 @@ def load_traffic():
         return None
 
 
-def ring_leg(lib, args, rank, world):
-    """pg_reduce_scatter over RCCL/xGMI, device-resident, BASELINE configs 3/4."""
+def ring_leg(lib, args, rank, world, transport):
+    """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3/4
+    shapes.  transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads)."""
     if world == 4:
         dt, count, cfg = pgamd.DT_INT32, 1 << 28, "config3: 4-GPU ring, int32 sum, 1 GiB/rank"
     elif world == 8:
@@ -233,7 +239,8 @@ def ring_leg(lib, args, rank, world):
     es = pgamd.ELEM_SIZE[dt]
     hosts = " ".join(["127.0.0.1"] * world).encode()
     os.environ["PG_RANK"] = str(rank)
-    os.environ.setdefault("PG_PORT", str(int(os.environ.get("MASTER_PORT", "29500")) + 17))
+    os.environ["PG_TRANSPORT"] = transport
+    os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + (17 if transport == "rccl" else 19))
     h = ctypes.c_void_p()
     if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
         raise RuntimeError("connect_process_group: " + pgamd.last_error())
@@ -265,7 +272,7 @@ def ring_leg(lib, args, rank, world):
                 "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
                 "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
                 "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
-                "transport": "rccl-p2p-xgmi"}
+                "transport": {"rccl": "RCCL P2P ring over xGMI", "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order"}[transport]}
     finally:
         lib.pg_close(h)
 
@@ -281,12 +288,6 @@ def main():
     achieved_gbs = bytes_per_step / (mean_launch_ms * 1e-3) / 1e9
     value = world * bytes_per_step * args.steps / wall_max / GIB
 
-    ring = None
-    if world > 1 and not args.no_ring:
-        try:
-            ring = ring_leg(lib, args, rank, world)
-        except Exception as e:  # the primary measurement stands on its own
-            ring = {"error": f"{type(e).__name__}: {e}"}
     cpu = None
     host = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -297,6 +298,7 @@ def main():
         except Exception as e:
             host = {"error": f"{type(e).__name__}: {e}"}
 
+    line = None
     if rank == 0:
         traffic = load_traffic()
         line = {
@@ -318,9 +320,37 @@ def main():
                          "bytes_per_launch": bytes_per_step},
             "cpu_baseline": cpu,
             "host_staged": host,
-            "ring": ring,
-            "kernel": pgamd.load().pgk_version().decode(),
+            "ring": None,
+            "kernel": lib.pgk_version().decode(),
         }
+
+    if world > 1 and not args.no_ring:
+        # the ring leg must never cost the primary line: a watchdog prints it
+        # and ends every rank if the ring (RCCL init, a transfer) stalls
+        import threading
+
+        ring = {}
+        if line is not None:
+            line["ring"] = ring        # filled in place: a watchdog print keeps finished legs
+
+        def _expire():
+            if line is not None:
+                ring["watchdog"] = f"ring leg exceeded {args.ring_timeout} s; unfinished transports omitted"
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        dog = threading.Timer(args.ring_timeout, _expire)
+        dog.daemon = True
+        dog.start()
+        for transport in args.transports.split(","):
+            try:
+                ring[transport] = ring_leg(lib, args, rank, world, transport)
+            except Exception as e:  # the primary measurement stands on its own
+                ring[transport] = {"error": f"{type(e).__name__}: {e}"}
+            barrier(world)
+        dog.cancel()
+
+    if line is not None:
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-/* struct pg.transport values.  Selected with PG_TRANSPORT=rccl|loopback. */
+/* struct pg.transport values.  Selected with PG_TRANSPORT=rccl|xgmi|loopback. */
 #define PG_TRANSPORT_RCCL     0  /* one process per GPU, RCCL P2P over xGMI (default) */
 #define PG_TRANSPORT_LOOPBACK 1  /* one process, the reference's single-process mock
                                     schedule (src/pg.c:161-179, :264-321) run on the
@@ -25,6 +25,10 @@ extern "C" {
                                     sharing one GPU; the hop is a device copy.  Used
                                     by pgx_sim_run() to exercise the ring executor   */
 #define PG_TRANSPORT_SELF     3  /* world_size == 1 */
+#define PG_TRANSPORT_XGMI     4  /* one process per GPU; each rank reads block r of every
+                                    peer's contribution directly over xGMI (HIP IPC) and
+                                    folds them in ring order with one kernel: all links
+                                    busy at once, results identical to the ring        */
 
 /* Ring block partition used by pg_reduce_scatter / pg_all_reduce: block b of
  * count elements = [b*B, min((b+1)*B, count)) with B = ceil(count/world), the

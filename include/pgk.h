@@ -43,6 +43,13 @@ int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *strea
 int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
                    void *stream);
 
+/* out[i] = ((srcs[0][i] op srcs[1][i]) op srcs[2][i]) ... op srcs[nsrc-1][i],
+ * folded left to right (1 <= nsrc <= 16).  Sources may be peer GPUs' memory
+ * mapped through HIP IPC (read over xGMI).  With srcs in ring order this is
+ * bit-identical to the W-1 ring steps of reduce_inplace it fuses. */
+int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
+                     void *stream);
+
 /* Device helpers for hosts that do not link HIP themselves (ctypes, cgo ...). */
 int pgk_device_count(int *count);
 int pgk_set_device(int device);

@@ -112,7 +112,10 @@ void pg_impl_destroy(struct pg *pg) {
   if (!im) return;
   if (im->comm) hipStreamSynchronize(im->comm);
   if (im->red) hipStreamSynchronize(im->red);
+  if (pg->transport == PG_TRANSPORT_XGMI) pg_xport_xgmi_destroy(pg);
   if (im->ops && im->ops->destroy) im->ops->destroy(im);
+  pg_boot_close(im->boot_fds, pg->world_size);
+  im->boot_fds = NULL;
   for (int i = 0; i < im->n_red_ev; ++i) hipEventDestroy(im->red_ev[i]);
   free(im->red_ev);
   for (int i = 0; i < PG_RECV_EVENTS; ++i) if (im->recv_ev[i]) hipEventDestroy(im->recv_ev[i]);
@@ -149,11 +152,13 @@ int connect_process_group(const char *serverlist, void **out_handle) {
   const char *tr = getenv("PG_TRANSPORT");
   if (pg->world_size == 1) pg->transport = PG_TRANSPORT_SELF;
   else if (tr && strcmp(tr, "loopback") == 0) pg->transport = PG_TRANSPORT_LOOPBACK;
+  else if (tr && strcmp(tr, "xgmi") == 0) pg->transport = PG_TRANSPORT_XGMI;
   else if (!tr || !*tr || strcmp(tr, "rccl") == 0) pg->transport = PG_TRANSPORT_RCCL;
-  else { pg_set_error("PG_TRANSPORT=%s: expected rccl or loopback", tr); goto fail; }
+  else { pg_set_error("PG_TRANSPORT=%s: expected rccl, xgmi or loopback", tr); goto fail; }
 
   if (pg_impl_create(pg)) goto fail;
   if (pg->transport == PG_TRANSPORT_RCCL && pg_xport_rccl_init(pg)) goto fail;
+  if (pg->transport == PG_TRANSPORT_XGMI && pg_xport_xgmi_init(pg)) goto fail;
   *out_handle = pg;
   return 0;
 fail:
@@ -353,6 +358,8 @@ int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype
     rc = copy_any(recvbuf, sendbuf, (size_t)count * pg_elem_size(datatype));
   else if (pg->transport == PG_TRANSPORT_LOOPBACK)
     rc = loopback_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg->transport == PG_TRANSPORT_XGMI)
+    rc = pg_xgmi_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;
@@ -431,6 +438,8 @@ int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, vo
     rc = sendbuf ? copy_any(recvbuf, sendbuf, (size_t)count * pg_elem_size(datatype)) : 0;
   else if (pg->transport == PG_TRANSPORT_LOOPBACK)
     rc = loopback_all_gather(pg, sendbuf, recvbuf, count, datatype);
+  else if (pg->transport == PG_TRANSPORT_XGMI)
+    rc = pg_xgmi_all_gather(pg, sendbuf, recvbuf, count, datatype);
   else
     rc = ring_all_gather(pg, sendbuf, recvbuf, count, datatype);
   im->stats.wall_us = now_us() - t;
@@ -497,7 +506,9 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
     pg_set_error("pg_all_reduce: the reference's world_size > 1 all-reduce writes past a "
                  "count-element recvbuf (src/pg.c:303,313-317); no defined result to reproduce");
     rc = -1;
-  } else
+  } else if (pg->transport == PG_TRANSPORT_XGMI)
+    rc = pg_xgmi_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
+  else
     rc = ring_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;
   return rc;

@@ -135,17 +135,32 @@ static int io_full(int fd, void *buf, size_t n, int writing) {
   return 0;
 }
 
-/* Rank 0 serves `blob` to every other rank over TCP; the others fetch it. */
-int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes) {
+/* ---- the bootstrap star ---------------------------------------------------------
+ * Rank 0 listens on PG_PORT and keeps one TCP connection per peer for the
+ * handle's lifetime; the others keep one connection to rank 0.  On it run the
+ * few host-side collectives the library needs (unique-id broadcast, IPC handle
+ * all-gather, barriers).  Retry/backoff and the 0xA5 ready token follow the
+ * reference's bootstrap (src/pg_net.c:298-436, :699-710). */
+
+static int tcp_nodelay(int fd) {
+  int one = 1;
+  return setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+}
+
+int pg_boot_open(struct pg *pg, int **fds_out) {
   int timeout_ms = PG_DEFAULT_CONNECT_TIMEOUT_MS, backoff_ms = PG_DEFAULT_BACKOFF_MS;
   env_int("PG_CONNECT_TIMEOUT_MS", &timeout_ms);
   env_int("PG_BACKOFF_MS", &backoff_ms);
+  int W = pg->world_size;
+  int *fds = (int *)malloc(sizeof(int) * (size_t)W);
+  if (!fds) return -1;
+  for (int i = 0; i < W; ++i) fds[i] = -1;
   char port[16];
   snprintf(port, sizeof(port), "%d", pg->port);
 
   if (pg->rank == 0) {
     int ls = socket(AF_INET, SOCK_STREAM, 0);
-    if (ls < 0) { pg_set_error("socket: %s", strerror(errno)); return -1; }
+    if (ls < 0) { pg_set_error("socket: %s", strerror(errno)); free(fds); return -1; }
     int one = 1;
     setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     struct sockaddr_in a;
@@ -153,31 +168,40 @@ int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes) {
     a.sin_family = AF_INET;
     a.sin_addr.s_addr = htonl(INADDR_ANY);
     a.sin_port = htons((uint16_t)pg->port);
-    if (bind(ls, (struct sockaddr *)&a, sizeof(a)) || listen(ls, pg->world_size)) {
+    if (bind(ls, (struct sockaddr *)&a, sizeof(a)) || listen(ls, W)) {
       pg_set_error("bootstrap listen on port %d: %s", pg->port, strerror(errno));
       close(ls);
+      free(fds);
       return -1;
     }
     long deadline = now_ms() + timeout_ms;
-    int served = 0;
-    while (served < pg->world_size - 1) {
+    int joined = 0;
+    while (joined < W - 1) {
       struct pollfd pfd = {ls, POLLIN, 0};
       long left = deadline - now_ms();
-      if (left <= 0) { pg_set_error("bootstrap: %d of %d ranks never connected", pg->world_size - 1 - served, pg->world_size - 1); close(ls); return -1; }
+      if (left <= 0) {
+        pg_set_error("bootstrap: %d of %d ranks never connected to port %d", W - 1 - joined, W - 1, pg->port);
+        close(ls);
+        pg_boot_close(fds, W);
+        return -1;
+      }
       int pr = poll(&pfd, 1, (int)left);
-      if (pr < 0 && errno == EINTR) continue;
       if (pr <= 0) continue;
       int c = accept(ls, NULL, NULL);
       if (c < 0) continue;
       int32_t peer = -1;
-      if (io_full(c, &peer, sizeof(peer), 0) == 0 && peer > 0 && peer < pg->world_size &&
-          io_full(c, blob, blob_bytes, 1) == 0) {
-        uint8_t ack = 0;
-        if (io_full(c, &ack, 1, 0) == 0 && ack == 0xA5) ++served;  /* ready token, cf. pg_net.c:699-710 */
+      uint8_t ack = 0xA5;
+      if (io_full(c, &peer, sizeof(peer), 0) == 0 && peer > 0 && peer < W && fds[peer] < 0 &&
+          io_full(c, &ack, 1, 1) == 0) {
+        tcp_nodelay(c);
+        fds[peer] = c;
+        ++joined;
+      } else {
+        close(c);
       }
-      close(c);
     }
     close(ls);
+    *fds_out = fds;
     return 0;
   }
 
@@ -186,19 +210,21 @@ int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes) {
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
   int gai = getaddrinfo(pg->hosts[0], port, &hints, &res);
-  if (gai != 0 || !res) { pg_set_error("bootstrap: resolve %s: %s", pg->hosts[0], gai_strerror(gai)); return -1; }
+  if (gai != 0 || !res) {
+    pg_set_error("bootstrap: resolve %s: %s", pg->hosts[0], gai_strerror(gai));
+    free(fds);
+    return -1;
+  }
   long deadline = now_ms() + timeout_ms;
-  int rc = -1;
   while (now_ms() < deadline) {
     int fd = socket(AF_INET, SOCK_STREAM, 0);
     if (fd < 0) break;
     if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
       int32_t me = pg->rank;
-      uint8_t ack = 0xA5;
-      if (io_full(fd, &me, sizeof(me), 1) == 0 && io_full(fd, blob, blob_bytes, 0) == 0 &&
-          io_full(fd, &ack, 1, 1) == 0) {
-        rc = 0;
-        close(fd);
+      uint8_t ack = 0;
+      if (io_full(fd, &me, sizeof(me), 1) == 0 && io_full(fd, &ack, 1, 0) == 0 && ack == 0xA5) {
+        tcp_nodelay(fd);
+        fds[0] = fd;
         break;
       }
     }
@@ -207,6 +233,51 @@ int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes) {
     nanosleep(&ts, NULL);
   }
   freeaddrinfo(res);
-  if (rc) pg_set_error("bootstrap: could not reach rank 0 at %s:%s within %d ms", pg->hosts[0], port, timeout_ms);
+  if (fds[0] < 0) {
+    pg_set_error("bootstrap: could not reach rank 0 at %s:%s within %d ms", pg->hosts[0], port, timeout_ms);
+    free(fds);
+    return -1;
+  }
+  *fds_out = fds;
+  return 0;
+}
+
+void pg_boot_close(int *fds, int n) {
+  if (!fds) return;
+  for (int i = 0; i < n; ++i) if (fds[i] >= 0) close(fds[i]);
+  free(fds);
+}
+
+/* all[q*bytes ..] = rank q's `mine`, on every rank. */
+int pg_boot_allgather(struct pg *pg, const int *fds, const void *mine, void *all, size_t bytes) {
+  int W = pg->world_size;
+  if (W == 1) { memcpy(all, mine, bytes); return 0; }
+  if (pg->rank == 0) {
+    memcpy(all, mine, bytes);
+    for (int q = 1; q < W; ++q)
+      if (io_full(fds[q], (char *)all + (size_t)q * bytes, bytes, 0)) {
+        pg_set_error("bootstrap allgather: lost rank %d", q);
+        return -1;
+      }
+    for (int q = 1; q < W; ++q)
+      if (io_full(fds[q], all, bytes * (size_t)W, 1)) {
+        pg_set_error("bootstrap allgather: lost rank %d", q);
+        return -1;
+      }
+    return 0;
+  }
+  if (io_full(fds[0], (void *)mine, bytes, 1) || io_full(fds[0], all, bytes * (size_t)W, 0)) {
+    pg_set_error("bootstrap allgather: lost rank 0");
+    return -1;
+  }
+  return 0;
+}
+
+int pg_boot_barrier(struct pg *pg, const int *fds) {
+  uint8_t me = 0xA5, all[256];
+  uint8_t *buf = pg->world_size <= 256 ? all : (uint8_t *)malloc((size_t)pg->world_size);
+  if (!buf) return -1;
+  int rc = pg_boot_allgather(pg, fds, &me, buf, 1);
+  if (buf != all) free(buf);
   return rc;
 }

@@ -66,6 +66,7 @@ struct pg_impl {
   void *dout;      size_t dout_cap;   /* device result / full buffer          */
 
   struct pg_step *steps; int steps_cap;
+  int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */
   struct pg_stats stats;
 };
 
@@ -82,6 +83,12 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
 
 /* pg_xport_rccl.c */
 int pg_xport_rccl_init(struct pg *pg);
+/* pg_xport_xgmi.c: direct peer reads over xGMI (IPC-mapped exchange buffers) */
+int pg_xport_xgmi_init(struct pg *pg);
+void pg_xport_xgmi_destroy(struct pg *pg);
+int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
+int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt);
+int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
 /* pg_xport_threads.c */
 int pg_xport_threads_attach(struct pg *pg, void *hub);
 
@@ -90,7 +97,10 @@ int pg_parse_hosts(const char *list, char ***hosts_out, int *n_out);
 int pg_discover_rank(char **hosts, int n, int *rank_out);
 int pg_discover_device(int rank, int *device_out);
 void pg_apply_env(struct pg *pg);
-int pg_boot_exchange(struct pg *pg, void *blob, size_t blob_bytes);
+int pg_boot_open(struct pg *pg, int **fds_out);
+void pg_boot_close(int *fds, int n);
+int pg_boot_allgather(struct pg *pg, const int *fds, const void *mine, void *all, size_t bytes);
+int pg_boot_barrier(struct pg *pg, const int *fds);
 
 #define PG_CHECK_HIP(expr)                                                          \
   do {                                                                              \

@@ -61,7 +61,12 @@ int pg_xport_rccl_init(struct pg *pg) {
   ncclUniqueId id;
   memset(&id, 0, sizeof(id));
   if (pg->rank == 0) PG_CHECK_NCCL(ncclGetUniqueId(&id));
-  if (pg_boot_exchange(pg, &id, sizeof(id))) return -1;
+  if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
+  ncclUniqueId *all = (ncclUniqueId *)malloc(sizeof(ncclUniqueId) * (size_t)pg->world_size);
+  if (!all) { pg_set_error("out of host memory"); return -1; }
+  if (pg_boot_allgather(pg, im->boot_fds, &id, all, sizeof(id))) { free(all); return -1; }
+  id = all[0];                                   /* rank 0's id, relayed */
+  free(all);
   ncclComm_t comm = NULL;
   PG_CHECK_NCCL(ncclCommInitRank(&comm, pg->world_size, id, pg->rank));
   im->xctx = comm;

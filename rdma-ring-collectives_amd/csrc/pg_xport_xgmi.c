@@ -1,0 +1,250 @@
+/*
+ * pg_xport_xgmi.c -- PG_TRANSPORT=xgmi: the reduce-scatter as direct reads of
+ * every peer's contribution over xGMI, folded in ring order by one kernel.
+ *
+ * The reference moves each chunk one hop per round and reduces it on arrival
+ * (ring design README.md:68-71; mocked at src/pg.c:277-289).  On one MI355X
+ * node every GPU has a direct xGMI link to each of its 7 peers, so rank r can
+ * read block r of all W contributions at once -- W-1 links busy instead of one
+ * -- and fold them in the exact order the ring would:
+ *     out = x[r+1] op x[r+2] op ... op x[r]        (indices mod W)
+ * which is bit-identical to the RCCL ring and to the oracle's ring simulator.
+ * This is the "fused receive-reduce" + "multi-link" rows of SURVEY.md §8f.
+ *
+ * Memory: each rank owns one IPC-exportable HBM allocation split into
+ * contribution slots X0/X1 and all-reduce result slots R0/R1 (double-buffered
+ * by call parity), mapped into every peer with hipIpcOpenMemHandle.  A call
+ * copies its input into X[parity], meets the others at a host barrier on the
+ * bootstrap star (pg_boot.c), then reads.  Double buffering makes one barrier
+ * per call enough: a slot is rewritten two calls later, and every rank passed
+ * the intervening call's barrier only after finishing its reads.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pg_impl.h"
+
+#define XG_SLOTS 4              /* X0, X1, R0, R1 */
+#define XG_GRANULE (64ull << 20)
+
+struct xgmi_ctx {
+  void *mem;                    /* my allocation: XG_SLOTS * cap bytes      */
+  size_t cap;                   /* bytes per slot                           */
+  void **peer;                  /* peer[q] = rank q's allocation, mapped    */
+  hipStream_t *cs;              /* one copy stream per source rank          */
+  unsigned long gen;            /* collective calls so far (slot parity)    */
+};
+
+static struct xgmi_ctx *ctx_of(struct pg *pg) {
+  return (struct xgmi_ctx *)((struct pg_impl *)pg->impl)->xctx;
+}
+
+static char *slot(struct xgmi_ctx *x, int q, int which) {
+  return (char *)x->peer[q] + (size_t)which * x->cap;
+}
+
+static void unmap(struct pg *pg, struct xgmi_ctx *x) {
+  if (!x->peer) return;
+  for (int q = 0; q < pg->world_size; ++q)
+    if (q != pg->rank && x->peer[q]) hipIpcCloseMemHandle(x->peer[q]);
+  memset(x->peer, 0, sizeof(void *) * (size_t)pg->world_size);
+  if (x->mem) hipFree(x->mem);
+  x->mem = NULL;
+  x->cap = 0;
+}
+
+/* Collective: every rank calls with the same `bytes` (same count), so every
+ * rank grows in the same call to the same size. */
+static int ensure(struct pg *pg, size_t bytes) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  if (bytes <= x->cap && x->mem) return 0;
+  size_t cap = x->cap ? x->cap : XG_GRANULE;
+  while (cap < bytes) cap *= 2;
+  /* nobody may still read the old slots */
+  if (x->mem && pg_boot_barrier(pg, im->boot_fds)) return -1;
+  unmap(pg, x);
+  PG_CHECK_HIP(hipMalloc(&x->mem, cap * XG_SLOTS));
+  x->cap = cap;
+  hipIpcMemHandle_t mine, *all = (hipIpcMemHandle_t *)malloc(sizeof(hipIpcMemHandle_t) * (size_t)pg->world_size);
+  if (!all) { pg_set_error("xgmi: out of host memory"); return -1; }
+  hipError_t e = hipIpcGetMemHandle(&mine, x->mem);
+  if (e != hipSuccess) { free(all); pg_set_error("xgmi: hipIpcGetMemHandle: %s", hipGetErrorString(e)); return -1; }
+  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) { free(all); return -1; }
+  for (int q = 0; q < pg->world_size; ++q) {
+    if (q == pg->rank) { x->peer[q] = x->mem; continue; }
+    e = hipIpcOpenMemHandle(&x->peer[q], all[q], hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      free(all);
+      pg_set_error("xgmi: hipIpcOpenMemHandle(rank %d): %s", q, hipGetErrorString(e));
+      return -1;
+    }
+  }
+  free(all);
+  return 0;
+}
+
+int pg_xport_xgmi_init(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  if (pg->world_size > 16) { pg_set_error("xgmi transport: at most 16 ranks"); return -1; }
+  struct xgmi_ctx *x = (struct xgmi_ctx *)calloc(1, sizeof(*x));
+  if (!x) return -1;
+  im->xctx = x;
+  x->peer = (void **)calloc((size_t)pg->world_size, sizeof(void *));
+  x->cs = (hipStream_t *)calloc((size_t)pg->world_size, sizeof(hipStream_t));
+  if (!x->peer || !x->cs) { pg_set_error("xgmi: out of host memory"); return -1; }
+  for (int q = 0; q < pg->world_size; ++q)
+    PG_CHECK_HIP(hipStreamCreateWithFlags(&x->cs[q], hipStreamNonBlocking));
+  if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
+  return pg_boot_barrier(pg, im->boot_fds);
+}
+
+void pg_xport_xgmi_destroy(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  if (!x) return;
+  /* peers may still be reading my last contribution: meet them first */
+  if (x->mem && im->boot_fds) pg_boot_barrier(pg, im->boot_fds);
+  unmap(pg, x);
+  if (x->cs)
+    for (int q = 0; q < pg->world_size; ++q) if (x->cs[q]) hipStreamDestroy(x->cs[q]);
+  free(x->cs);
+  free(x->peer);
+  free(x);
+  im->xctx = NULL;
+}
+
+static int is_dev(const void *p) {
+  if (!p) return 0;
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof(a));
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
+}
+
+/* Copy this rank's contribution into X[parity] and meet the other ranks. */
+static int publish(struct pg *pg, const void *src, size_t bytes, int src_dev, char **xslot) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  int which = (int)(x->gen & 1);
+  *xslot = slot(x, pg->rank, which);
+  if (src_dev) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  if (bytes) {
+    PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                im->red));
+    PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  }
+  return pg_boot_barrier(pg, im->boot_fds);
+}
+
+/* out = fold over ranks, in ring order, of block `b` of slot `which`. */
+static int fold_block(struct pg *pg, void *out, int which, size_t off_elems, size_t len, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  if (!len) return 0;
+  int W = pg->world_size, r = pg->rank;
+  size_t es = pg_elem_size(dt);
+  const void *srcs[16];
+  for (int j = 0; j < W; ++j) srcs[j] = slot(x, (r + 1 + j) % W, which) + off_elems * es;
+  if (pgk_reduce_multi(out, srcs, W, len, dt, op, (void *)im->red)) {
+    pg_set_error("xgmi: %s", pgk_last_error());
+    return -1;
+  }
+  im->stats.reduce_launches += 1;
+  im->stats.reduce_elems += (int64_t)len * (W - 1);
+  im->stats.bytes_recv += (int64_t)(len * es) * (W - 1);
+  return 0;
+}
+
+int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
+  pg_block_range(count, pg->world_size, pg->rank, &off, &len);
+  if (ensure(pg, bytes)) return -1;
+  int rd = is_dev(recvbuf);
+  char *xs;
+  if (publish(pg, sendbuf, bytes, is_dev(sendbuf), &xs)) return -1;
+  void *out = recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, len * es)) return -1;
+    out = im->dout;
+  }
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
+  if (fold_block(pg, out, (int)(x->gen & 1), off, len, dt, op)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->red));
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
+  if (!rd && len) PG_CHECK_HIP(hipMemcpy(recvbuf, out, len * es, hipMemcpyDeviceToHost));
+  x->gen++;
+  return 0;
+}
+
+/* Gather: copy block q (elements [off(q), off(q)+len(q)) of slot `which` of
+ * rank q) into full + off(q), all ranks' copies concurrently. */
+static int gather(struct pg *pg, char *full, int which, int count, int uniform, int dt) {
+  struct xgmi_ctx *x = ctx_of(pg);
+  size_t es = pg_elem_size(dt);
+  for (int q = 0; q < pg->world_size; ++q) {
+    size_t off, len;
+    if (uniform) { off = (size_t)q * (size_t)count; len = (size_t)count; }
+    else pg_block_range(count, pg->world_size, q, &off, &len);
+    if (!len) continue;
+    const char *src = slot(x, q, which) + (uniform ? 0 : off * es);
+    PG_CHECK_HIP(hipMemcpyAsync(full + off * es, src, len * es, hipMemcpyDeviceToDevice, x->cs[q]));
+  }
+  for (int q = 0; q < pg->world_size; ++q) PG_CHECK_HIP(hipStreamSynchronize(x->cs[q]));
+  return 0;
+}
+
+int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  size_t es = pg_elem_size(dt), slot_bytes = (size_t)count * es, total = slot_bytes * (size_t)pg->world_size;
+  if (ensure(pg, slot_bytes)) return -1;
+  int rd = is_dev(recvbuf);
+  const void *mine = sendbuf ? sendbuf : (const char *)recvbuf + (size_t)pg->rank * slot_bytes;
+  char *xs;
+  if (publish(pg, mine, slot_bytes, sendbuf ? is_dev(sendbuf) : rd, &xs)) return -1;
+  char *full = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
+    full = (char *)im->dout;
+  }
+  if (gather(pg, full, (int)(x->gen & 1), count, 1, dt)) return -1;
+  if (!rd && total) PG_CHECK_HIP(hipMemcpy(recvbuf, full, total, hipMemcpyDeviceToHost));
+  im->stats.bytes_recv += (int64_t)(total - slot_bytes);
+  x->gen++;
+  return 0;
+}
+
+int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
+  pg_block_range(count, pg->world_size, pg->rank, &off, &len);
+  if (ensure(pg, bytes)) return -1;
+  int rd = is_dev(recvbuf), which = (int)(x->gen & 1);
+  char *xs;
+  if (publish(pg, sendbuf, bytes, is_dev(sendbuf), &xs)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
+  /* my block of the result goes to R[which] so that every rank can gather it */
+  if (fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, which, off, len, dt, op)) return -1;
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (pg_boot_barrier(pg, im->boot_fds)) return -1;
+  char *full = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
+    full = (char *)im->dout;
+  }
+  if (gather(pg, full, 2 + which, count, 0, dt)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->red));
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
+  if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
+  x->gen++;
+  return 0;
+}

@@ -113,6 +113,60 @@ __global__ __launch_bounds__(kScalarBlock) void k_reduce_scalar(T* __restrict__ 
     out[i] = apply<OP>(a[i], b[i]);
 }
 
+// Multi-source fold: out[i] = ((s0[i] op s1[i]) op s2[i]) ... op s[k-1][i], left
+// to right, each source a different rank's buffer (IPC-mapped peer memory over
+// xGMI, or local).  One element sees exactly the operation sequence the ring
+// would apply, so the result is bit-identical to a W-step ring reduction in
+// the same order.  Sources are passed by value in the kernel arguments.
+constexpr int kMaxSrc = 16;
+constexpr int kMultiBlock = 256;
+template <typename T>
+struct SrcList {
+  const T* p[kMaxSrc];
+};
+
+template <typename T, int OP, int NS>
+__global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_vec(T* __restrict__ out, SrcList<T> src,
+                                                                  int nsrc, unsigned head, size_t nvec,
+                                                                  unsigned tail) {
+  using V = typename VecOf<T>::type;
+  constexpr int W = VecOf<T>::width;
+  const int k = NS ? NS : nsrc;
+  if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+    size_t e = threadIdx.x < head ? threadIdx.x : head + nvec * W + (threadIdx.x - head);
+    T acc = src.p[0][e];
+    for (int j = 1; j < k; ++j) acc = apply<OP>(acc, src.p[j][e]);
+    out[e] = acc;
+  }
+  const size_t stride = (size_t)gridDim.x * kMultiBlock;
+  for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < nvec; i += stride) {
+    if constexpr (NS > 0) {
+      V x[NS];
+#pragma unroll
+      for (int j = 0; j < NS; ++j) x[j] = ld<true>(reinterpret_cast<const V*>(src.p[j] + head) + i);
+      V acc = x[0];
+#pragma unroll
+      for (int j = 1; j < NS; ++j) acc = apply<OP>(acc, x[j]);
+      st<true>(reinterpret_cast<V*>(out + head) + i, acc);
+    } else {
+      V acc = ld<true>(reinterpret_cast<const V*>(src.p[0] + head) + i);
+      for (int j = 1; j < k; ++j) acc = apply<OP>(acc, ld<true>(reinterpret_cast<const V*>(src.p[j] + head) + i));
+      st<true>(reinterpret_cast<V*>(out + head) + i, acc);
+    }
+  }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_scalar(T* __restrict__ out, SrcList<T> src,
+                                                                     int nsrc, size_t n) {
+  const size_t stride = (size_t)gridDim.x * kMultiBlock;
+  for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < n; i += stride) {
+    T acc = src.p[0][i];
+    for (int j = 1; j < nsrc; ++j) acc = apply<OP>(acc, src.p[j][i]);
+    out[i] = acc;
+  }
+}
+
 // ---- host side ---------------------------------------------------------------
 
 thread_local char g_err[256] = "";
@@ -245,9 +299,71 @@ int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, vo
   return 0;
 }
 
+template <typename T, int OP>
+hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s) {
+  SrcList<T> sl{};
+  uintptr_t m = (uintptr_t)out & 15;
+  bool congruent = (m % sizeof(T)) == 0;
+  for (int j = 0; j < nsrc; ++j) {
+    sl.p[j] = srcs[j];
+    if (((uintptr_t)srcs[j] & 15) != m) congruent = false;
+  }
+  const size_t W = 16 / sizeof(T);
+  if (congruent) {
+    size_t head = m ? (16 - m) / sizeof(T) : 0;
+    if (head > n) head = n;
+    size_t nvec = (n - head) / W, tail = (n - head) % W;
+    size_t g = (nvec + kMultiBlock - 1) / kMultiBlock;
+    if (g == 0) g = 1;
+    if (g > 0x7fffffff) g = 0x7fffffff;
+    dim3 grid((unsigned)g), block(kMultiBlock);
+    switch (nsrc) {
+#define PGK_MULTI_CASE(K) \
+      case K: hipLaunchKernelGGL((k_reduce_multi_vec<T, OP, K>), grid, block, 0, s, out, sl, nsrc, \
+                                 (unsigned)head, nvec, (unsigned)tail); break;
+      PGK_MULTI_CASE(1) PGK_MULTI_CASE(2) PGK_MULTI_CASE(3) PGK_MULTI_CASE(4)
+      PGK_MULTI_CASE(5) PGK_MULTI_CASE(6) PGK_MULTI_CASE(7) PGK_MULTI_CASE(8)
+#undef PGK_MULTI_CASE
+      default:
+        hipLaunchKernelGGL((k_reduce_multi_vec<T, OP, 0>), grid, block, 0, s, out, sl, nsrc, (unsigned)head,
+                           nvec, (unsigned)tail);
+    }
+  } else {
+    size_t g = (n + kMultiBlock - 1) / kMultiBlock;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP>), dim3((unsigned)g), dim3(kMultiBlock), 0, s, out, sl,
+                       nsrc, n);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
+
+int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
+  if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
+  if (n == 0) return 0;
+  if (!out || !srcs) { set_err("pgk: NULL buffer with n=%zu", n); return -1; }
+  for (int j = 0; j < nsrc; ++j)
+    if (!srcs[j]) { set_err("pgk: NULL source %d", j); return -1; }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (dt == PGK_DT_INT32) {
+    const uint32_t* const* x = (const uint32_t* const*)srcs;
+    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s)
+                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s);
+  } else {
+    const double* const* x = (const double* const*)srcs;
+    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s)
+                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s);
+  }
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
 
 int pgk_reduce(void* dst, const void* src, size_t n, int dt, int op, void* stream) {
   return launch(dst, dst, src, n, dt, op, stream);

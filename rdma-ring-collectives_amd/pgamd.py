@@ -22,7 +22,7 @@ REPO_ROOT = PKG_DIR.parent
 DT_INT32, DT_DOUBLE = 0, 1
 OP_SUM, OP_PROD = 0, 1
 # include/pg_ext.h
-PG_TRANSPORT_RCCL, PG_TRANSPORT_LOOPBACK, PG_TRANSPORT_THREADS, PG_TRANSPORT_SELF = 0, 1, 2, 3
+PG_TRANSPORT_RCCL, PG_TRANSPORT_LOOPBACK, PG_TRANSPORT_THREADS, PG_TRANSPORT_SELF, PG_TRANSPORT_XGMI = 0, 1, 2, 3, 4
 PG_BUF_NONE, PG_BUF_SRC, PG_BUF_OUT, PG_BUF_STAGE0, PG_BUF_STAGE1 = 0, 1, 2, 3, 4
 PG_COLL_REDUCE_SCATTER, PG_COLL_ALL_GATHER, PG_COLL_ALL_REDUCE = 0, 1, 2
 
@@ -89,6 +89,7 @@ _SIGS = {
     # include/pgk.h
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
+    "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_device_count": (_I, [ctypes.POINTER(_I)]),
     "pgk_set_device": (_I, [_I]),
     "pgk_synchronize": (_I, []),

@@ -164,3 +164,26 @@ def test_reduce_host_staged(gpu, lib, oracle):
     assert lib.pgx_reduce_host(None, None, 0, 1, 0, 0) == 0
     assert lib.pgx_reduce_host(None, None, 5, 1, 0, 0) == -1
     assert lib.pgx_reduce_host(None, None, 5, 3, 0, 0) == -1
+
+
+@pytest.mark.parametrize("dt,op", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_reduce_multi_fold_order(gpu, lib, oracle, dt, op):
+    """pgk_reduce_multi folds left to right: equal to nsrc-1 successive
+    reduce_inplace steps (the ring's per-element operation sequence)."""
+    import ctypes
+    torch = gpu
+    for nsrc in (1, 2, 3, 5, 8, 9, 16):
+        for n, shift in ((4099, 0), (1 << 18, 0), (1001, 1)):
+            xs = [oracle.fill(n + 2, dt, op, 900 + 31 * nsrc + j) for j in range(nsrc)]
+            want = xs[0][shift:shift + n].copy()
+            for j in range(1, nsrc):
+                want = oracle.reduce(want, xs[j][shift:shift + n], dt, op)
+            D = [to_dev(torch, x) for x in xs]
+            es = 4 if dt == 0 else 8
+            out = torch.zeros(n + 2, dtype=D[0].dtype, device="cuda")
+            srcs = (ctypes.c_void_p * nsrc)(*[ptr(d) + shift * es for d in D])
+            assert lib.pgk_reduce_multi(ptr(out), srcs, nsrc, n, dt, op, stream(torch)) == 0
+            assert to_host(torch, out)[:n].tobytes() == want.tobytes(), (nsrc, n, shift)
+    srcs = (ctypes.c_void_p * 17)()
+    assert lib.pgk_reduce_multi(ptr(out), srcs, 17, 4, dt, op, stream(torch)) == -1
+    assert lib.pgk_reduce_multi(ptr(out), srcs, 0, 4, dt, op, stream(torch)) == -1

@@ -1,0 +1,116 @@
+"""PG_TRANSPORT=xgmi with REAL separate processes (one rank per process) on the
+one GPU of the test box: IPC-mapped exchange buffers, the bootstrap star, the
+multi-source fold kernel and the public pg_* calls, end to end.  Every rank
+checks its results bit for bit against the oracle's ring simulator (same fold
+order as the RCCL ring)."""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+CASES = [  # coll, dt, op, count, on_dev, in_place
+    ("rs", 1, 0, 1000, True, False), ("rs", 0, 1, 4099, False, False), ("rs", 1, 1, 1, True, False),
+    ("rs", 0, 0, 0, True, False), ("rs", 1, 0, (1 << 20) + 3, True, False),
+    ("ag", 1, 0, 257, True, False), ("ag", 0, 0, 64, False, False), ("ag", 1, 0, 33, True, True),
+    ("ar", 1, 0, 100003, True, False), ("ar", 0, 1, 999, False, False), ("ar", 1, 1, 4096, True, True),
+    ("ar", 0, 0, 7, False, True), ("rs", 1, 0, 5000, True, False),
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_CONNECT_TIMEOUT_MS="120000")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        hosts = " ".join(["127.0.0.1"] * world).encode()
+        if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
+            q.put((rank, ["connect: " + pgamd.last_error()]))
+            return
+        hd = pgamd.head(h)
+        assert (hd.rank, hd.world_size, hd.transport) == (rank, world, pgamd.PG_TRANSPORT_XGMI)
+        NP = {0: np.int32, 1: np.float64}
+        for i, (coll, dt, op, count, on_dev, in_place) in enumerate(CASES):
+            xs = [orc.fill(count, dt, op, 700 + 13 * i + r) for r in range(world)]
+            if coll == "rs":
+                want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+                recv = np.zeros(max(want.size, 1), NP[dt])
+            elif coll == "ag":
+                want = orc.ring_all_gather(xs, dt)[rank]
+                recv = np.zeros(count * world, NP[dt])
+                if in_place:
+                    recv[rank * count:(rank + 1) * count] = xs[rank]
+            else:
+                want = orc.ring_all_reduce(xs, dt, op)[rank]
+                recv = xs[rank].copy() if in_place else np.zeros(count, NP[dt])
+            send = xs[rank] if xs[rank].size else np.zeros(1, NP[dt])
+            if on_dev:
+                S = torch.from_numpy(send.copy()).cuda()
+                R = torch.from_numpy(recv.copy() if recv.size else np.zeros(1, NP[dt])).cuda()
+                sp, rp = S.data_ptr(), R.data_ptr()
+            else:
+                S, R = send.copy(), recv.copy() if recv.size else np.zeros(1, NP[dt])
+                sp, rp = S.ctypes.data, R.ctypes.data
+            if coll == "rs":
+                rc = lib.pg_reduce_scatter(sp, rp, count, dt, op, h)
+            elif coll == "ag":
+                rc = lib.pg_all_gather(None if in_place else sp, rp, count, dt, h)
+            else:
+                rc = lib.pg_all_reduce(rp if in_place else sp, rp, count, dt, op, h)
+            if rc != 0:
+                fails.append((i, "rc", pgamd.last_error()))
+                break
+            got = R.cpu().numpy() if on_dev else R
+            if got[:want.size].tobytes() != want.tobytes():
+                fails.append((i, coll, dt, op, count, on_dev, in_place))
+        lib.pg_close(h)
+    except Exception as e:  # report, never hang the parent
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_xgmi_multiprocess(gpu, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=420))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
