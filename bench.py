@@ -227,9 +227,46 @@ def load_traffic():
         return None
 
 
+def _timed_rs(lib, h, x, out, count, dt, op, reps, world):
+    pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, op, h), "ring RS")   # warm
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, op, h), "ring RS")
+    barrier(world)
+    return max_over_ranks(time.perf_counter() - t0, world) / reps
+
+
+def _pattern(count, rank, world, dt, op):
+    """Inputs whose W-rank reduction is exact in both dtypes, so every rank can
+    check its block on the device: sum -> (i % 1000) + rank; prod -> powers of
+    two (double) / {1, 2, -1} (int32)."""
+    tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
+    i = torch.arange(count, device="cuda", dtype=torch.int64)
+    if op == pgamd.OP_SUM:
+        return ((i % 1000) + rank).to(tdt)
+    k = (i + rank) % 3
+    if dt == pgamd.DT_DOUBLE:
+        return torch.pow(2.0, (k - 1).to(torch.float64))
+    return torch.where(k == 2, -1, k + 1).to(torch.int32)
+
+
+def _expected_block(count, off, ln, world, dt, op):
+    tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
+    acc = None
+    for q in range(world):
+        v = _pattern(count, q, world, dt, op)[off:off + ln].to(torch.float64 if dt == pgamd.DT_DOUBLE else torch.int64)
+        acc = v if acc is None else (acc + v if op == pgamd.OP_SUM else acc * v)
+    if dt == pgamd.DT_INT32:
+        acc = ((acc + 2**31) % 2**32 - 2**31)
+    return acc.to(tdt)
+
+
 def ring_leg(lib, args, rank, world, transport):
-    """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3/4
-    shapes.  transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads)."""
+    """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3-5.
+    transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads).
+    Rows of the sweeps follow the reference's CSV discipline (README.md:85):
+    size, rounds, inflight, time_us, GB/s (GB/s = payload bytes per rank / time)."""
     if world == 4:
         dt, count, cfg = pgamd.DT_INT32, 1 << 28, "config3: 4-GPU ring, int32 sum, 1 GiB/rank"
     elif world == 8:
@@ -245,34 +282,74 @@ def ring_leg(lib, args, rank, world, transport):
     if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
         raise RuntimeError("connect_process_group: " + pgamd.last_error())
     try:
-        tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
-        idx = torch.arange(count, device="cuda", dtype=torch.int64) % 1000
-        x = (idx + rank).to(tdt)
+        hd = pgamd.head(h)
+        res = {"workload": cfg, "transport": {"rccl": "RCCL P2P ring over xGMI",
+                                              "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order"}[transport]}
+        x = _pattern(count, rank, world, dt, pgamd.OP_SUM)
         off, ln = pgamd.block_range(count, world, rank)
-        out = torch.empty(ln, dtype=tdt, device="cuda")
+        out = torch.empty(max(ln, 1), dtype=x.dtype, device="cuda")
         torch.cuda.synchronize()
-        # correctness probe: block r of sum_q (i % 1000 + q) = W*(i % 1000) + W(W-1)/2
         pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h), "ring RS")
-        want = (idx[off:off + ln] * world + world * (world - 1) // 2).to(tdt)
-        ok = bool(torch.equal(out, want))
-        del want, idx
+        ok = bool(torch.equal(out[:ln], _expected_block(count, off, ln, world, dt, pgamd.OP_SUM)))
+        res["ok"] = sum_over_ranks(1.0 if ok else 0.0, world) == world
+        wall = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, args.ring_steps, world)
+        payload = count * es                       # per rank
+        res.update({"ms_per_reduce_scatter": round(wall * 1e3, 3),
+                    "algbw_gibs": round(payload / wall / GIB, 2),
+                    "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
+                    "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
+                    "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight)})
+        # host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)
+        xh = x.cpu().numpy()
+        oh = np.empty(max(ln, 1), dtype=xh.dtype)
         barrier(world)
         t0 = time.perf_counter()
-        ring_us = []
-        for _ in range(args.ring_steps):
-            pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h), "ring RS")
-            ring_us.append(pgamd.stats(h)["ring_us"])
+        pgamd.check(lib.pg_reduce_scatter(xh.ctypes.data, oh.ctypes.data, count, dt, pgamd.OP_SUM, h), "host RS")
         barrier(world)
-        wall = max_over_ranks(time.perf_counter() - t0, world) / args.ring_steps
-        hd = pgamd.head(h)
-        ok_all = sum_over_ranks(1.0 if ok else 0.0, world) == world
-        payload = count * es                       # per rank
-        return {"workload": cfg, "ok": ok_all, "ms_per_reduce_scatter": round(wall * 1e3, 3),
-                "algbw_gibs": round(payload / wall / GIB, 2),
-                "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
-                "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
-                "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
-                "transport": {"rccl": "RCCL P2P ring over xGMI", "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order"}[transport]}
+        th = max_over_ranks(time.perf_counter() - t0, world)
+        res["host_buffers_ms"] = round(th * 1e3, 2)
+        res["host_buffers_ok"] = sum_over_ranks(1.0 if np.array_equal(oh[:ln], out[:ln].cpu().numpy()) else 0.0,
+                                                world) == world
+        del xh, oh
+        rounds = world - 1
+        if world == 4:                                    # config 3: PG_CHUNK_BYTES sweep
+            rows = []
+            for cb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20):
+                hd.chunk_bytes = cb
+                t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
+                rows.append([payload, rounds, int(hd.inflight), round(t * 1e6, 1), round(payload / t / 1e9, 2),
+                             cb])
+            hd.chunk_bytes = 4 << 20
+            res["chunk_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes"],
+                                  "rows": rows}
+        if world == 8:                                    # config 4: PG_INFLIGHT sweep
+            rows = []
+            for inf in (1, 2, 4, 8, 16):
+                hd.inflight = inf
+                t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
+                rows.append([payload, rounds, inf, round(t * 1e6, 1), round(payload / t / 1e9, 2)])
+            hd.inflight = 4
+            res["inflight_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s"], "rows": rows}
+        del x, out
+        torch.cuda.empty_cache()
+        if world == 8:                                    # config 5: prod, eager and 2 GiB mixed
+            cfg5 = []
+            for dt5, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
+                small = 4096 // pgamd.ELEM_SIZE[dt5]
+                for cnt in (small, big, small):
+                    xv = _pattern(cnt, rank, world, dt5, pgamd.OP_PROD)
+                    o5, l5 = pgamd.block_range(cnt, world, rank)
+                    ov = torch.empty(max(l5, 1), dtype=xv.dtype, device="cuda")
+                    reps = 20 if cnt == small else 2
+                    t = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
+                    good = bool(torch.equal(ov[:l5], _expected_block(cnt, o5, l5, world, dt5, pgamd.OP_PROD)))
+                    good = sum_over_ranks(1.0 if good else 0.0, world) == world
+                    cfg5.append({"dtype": "f64" if dt5 == pgamd.DT_DOUBLE else "i32", "count": cnt,
+                                 "bytes": cnt * pgamd.ELEM_SIZE[dt5], "time_us": round(t * 1e6, 1), "ok": good})
+                    del xv, ov
+                    torch.cuda.empty_cache()
+            res["config5_prod_mixed"] = cfg5
+        return res
     finally:
         lib.pg_close(h)
 
