@@ -20,6 +20,10 @@
 #ifndef PG_H
 #define PG_H
 
+#ifndef PG_API
+#define PG_API __attribute__((visibility("default")))
+#endif
+
 #include <stddef.h>
 #include <stdint.h>
 
@@ -63,27 +67,27 @@ typedef enum {
  * (or RANK) if set, else the position of gethostname() in the list (reference
  * behaviour).  Device: PG_DEVICE, else LOCAL_RANK, else rank % device count.
  * On success *out_handle receives a struct pg*.                 (ref pg.h:99) */
-int connect_process_group(const char *serverlist, void **out_handle);
+PG_API int connect_process_group(const char *serverlist, void **out_handle);
 
 /* Release everything the handle owns.  NULL-safe; always returns 0. (ref :107) */
-int pg_close(void *pg_handle);
+PG_API int pg_close(void *pg_handle);
 
 /* recvbuf[0..count) = reduction over all ranks of sendbuf[0..count).
  * In place iff sendbuf == recvbuf.                                 (ref :123) */
-int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype,
+PG_API int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype,
                   OPERATION op, void *pg_handle);
 
 /* Reduce sendbuf[0..count) over all ranks and leave block `rank` of the result
  * in recvbuf[0 .. block_len).  Blocks: ceil(count/world_size) elements each,
  * the last ones clamped to count (include/pg_ext.h: pg_block_range).
  * world_size == 1 copies count elements, as the reference does.    (ref :140) */
-int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count,
+PG_API int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count,
                       DATATYPE datatype, OPERATION op, void *pg_handle);
 
 /* recvbuf[q*count .. (q+1)*count) = sendbuf of rank q, on every rank.
  * sendbuf may be NULL when this rank's slot of recvbuf already holds its
  * contribution.                                                    (ref :156) */
-int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype,
+PG_API int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype,
                   void *pg_handle);
 
 #ifdef __cplusplus

@@ -9,6 +9,10 @@
 #ifndef PG_EXT_H
 #define PG_EXT_H
 
+#ifndef PG_API
+#define PG_API __attribute__((visibility("default")))
+#endif
+
 #include <stddef.h>
 #include <stdint.h>
 
@@ -33,7 +37,7 @@ extern "C" {
 /* Ring block partition used by pg_reduce_scatter / pg_all_reduce: block b of
  * count elements = [b*B, min((b+1)*B, count)) with B = ceil(count/world), the
  * reference's chunk_offsets() clamping (src/pg.c:126-138).  Elements. */
-int pg_block_range(int count, int world, int block, size_t *off, size_t *len);
+PG_API int pg_block_range(int count, int world, int block, size_t *off, size_t *len);
 
 /* Buffer roles named by plan steps. */
 #define PG_BUF_NONE   0
@@ -66,7 +70,7 @@ struct pg_step {
  * `inflight` segments per batch.  out_aliases_src: OUT is block `rank` of
  * SRC (in-place all-reduce).  Returns the number of steps written (or needed,
  * when steps == NULL), -1 on bad arguments. */
-int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
+PG_API int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
                            size_t chunk_bytes, size_t eager_max, int inflight,
                            int out_aliases_src, struct pg_step *steps, int max_steps);
 
@@ -74,13 +78,13 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
  * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole blocks, no reduce.
  * uniform = 1: blocks of `count` elements (pg_all_gather);
  * uniform = 0: the reduce-scatter partition of `count` (pg_all_reduce). */
-int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform,
+PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform,
                        struct pg_step *steps, int max_steps);
 
 /* Open a handle without a server list: transport LOOPBACK (reference mock
  * semantics for a given rank/world) or SELF (world must be 1).  The device is
  * the current HIP device. */
-int pg_connect_local(int rank, int world, int transport, void **out_handle);
+PG_API int pg_connect_local(int rank, int world, int transport, void **out_handle);
 
 /* Run one collective over `world` virtual ranks in this process (transport
  * THREADS): rank r uses sendbufs[r] / recvbufs[r] (HIP device or host
@@ -88,7 +92,7 @@ int pg_connect_local(int rank, int world, int transport, void **out_handle);
 #define PG_COLL_REDUCE_SCATTER 0
 #define PG_COLL_ALL_GATHER     1
 #define PG_COLL_ALL_REDUCE     2
-int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbufs,
+PG_API int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbufs,
                 int count, int datatype, int op, size_t chunk_bytes,
                 size_t eager_max, int inflight);
 
@@ -96,7 +100,7 @@ int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbuf
  * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces on two
  * streams (copies of one piece overlap the reduce of the previous one).
  * Synchronous.  This is what the PCIe-inclusive rate in DESIGN.md measures. */
-int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
+PG_API int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
 
 /* Measurements of the last collective on this handle. */
 struct pg_stats {
@@ -107,10 +111,16 @@ struct pg_stats {
   int64_t reduce_elems;  /* elements reduced by this rank                   */
   int64_t bytes_sent, bytes_recv;
 };
-int pg_get_stats(void *pg_handle, struct pg_stats *out);
+PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
+
+/* The TCP bootstrap star on its own (no GPU): join the ranks of `serverlist`
+ * through hosts[0]:port, all-gather one int per rank into out[world], meet at
+ * a barrier, disconnect.  Exercises the rank-0 relay that carries the RCCL
+ * unique id and the xgmi IPC handles. */
+PG_API int pgx_boot_selftest(const char *serverlist, int rank, int port, int value, int *out);
 
 /* Last error message of the calling thread ("" if none). */
-const char *pg_last_error(void);
+PG_API const char *pg_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,10 @@
 #ifndef PGK_H
 #define PGK_H
 
+#ifndef PG_API
+#define PG_API __attribute__((visibility("default")))
+#endif
+
 #include <stddef.h>
 
 #ifdef __cplusplus
@@ -36,53 +40,53 @@ extern "C" {
  * results are bit-identical to the reference loop for every non-NaN result.
  * dst and src must not partially overlap (dst == src is allowed).
  * n == 0 is a no-op returning 0.  dt/op outside the values above -> -1. */
-int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *stream);
+PG_API int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *stream);
 
 /* out[i] = a[i] op b[i] (out may equal a or b).  Same numerics as pgk_reduce;
  * used where the ring must not modify the caller's send buffer. */
-int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
+PG_API int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
                    void *stream);
 
 /* out[i] = ((srcs[0][i] op srcs[1][i]) op srcs[2][i]) ... op srcs[nsrc-1][i],
  * folded left to right (1 <= nsrc <= 16).  Sources may be peer GPUs' memory
  * mapped through HIP IPC (read over xGMI).  With srcs in ring order this is
  * bit-identical to the W-1 ring steps of reduce_inplace it fuses. */
-int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
+PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                      void *stream);
 
 /* Device helpers for hosts that do not link HIP themselves (ctypes, cgo ...). */
-int pgk_device_count(int *count);
-int pgk_set_device(int device);
-int pgk_synchronize(void);
+PG_API int pgk_device_count(int *count);
+PG_API int pgk_set_device(int device);
+PG_API int pgk_synchronize(void);
 
 /* Launch tuning, process-wide.  blocks_per_cu: grid cap = CUs x blocks_per_cu
  * (0 = uncapped one-shot grid, <0 = keep).  nontemporal: 1 = nt loads/stores,
  * 0 = default cache policy, <0 = keep.  Defaults are the measured best
  * (DESIGN.md). */
-int pgk_tune(int blocks_per_cu, int nontemporal);
+PG_API int pgk_tune(int blocks_per_cu, int nontemporal);
 
 /* Vector-kernel shape: threads per block x 16-byte vectors per operand each
  * thread keeps in flight.  Instantiated: 256x2, 256x4, 256x8, 512x2, 1024x1. */
-int pgk_tune_shape(int block, int unroll);
+PG_API int pgk_tune_shape(int block, int unroll);
 
 /* pgk_reduce, with the kernel's own begin/end timestamps recorded into two
  * HIP events (hipEvent_t as void*, from pgk_event_create) through
  * hipExtLaunchKernelGGL: their elapsed time is the kernel's execution, without
  * the dispatch overhead of separate event markers.  Used by bench.py. */
-int pgk_reduce_timed(void *dst, const void *src, size_t n, int dt, int op, void *stream,
+PG_API int pgk_reduce_timed(void *dst, const void *src, size_t n, int dt, int op, void *stream,
                      void *start_event, void *stop_event);
-int pgk_event_create(void **event);
-int pgk_event_destroy(void *event);
-int pgk_event_elapsed_ms(void *start_event, void *stop_event, float *ms);
+PG_API int pgk_event_create(void **event);
+PG_API int pgk_event_destroy(void *event);
+PG_API int pgk_event_elapsed_ms(void *start_event, void *stop_event, float *ms);
 
 /* Grid the next pgk_reduce of n elements of dt would launch (for bench/tests). */
-int pgk_launch_geometry(size_t n, int dt, unsigned *grid, unsigned *block);
+PG_API int pgk_launch_geometry(size_t n, int dt, unsigned *grid, unsigned *block);
 
 /* Last error message of the calling thread ("" if none). */
-const char *pgk_last_error(void);
+PG_API const char *pgk_last_error(void);
 
 /* Build identification, e.g. "pgk gfx950 hip-7.2". */
-const char *pgk_version(void);
+PG_API const char *pgk_version(void);
 
 #ifdef __cplusplus
 }

@@ -281,3 +281,22 @@ int pg_boot_barrier(struct pg *pg, const int *fds) {
   if (buf != all) free(buf);
   return rc;
 }
+
+/* Test hook (include/pg_ext.h): the bootstrap star without any GPU. */
+int pgx_boot_selftest(const char *serverlist, int rank, int port, int value, int *out) {
+  if (!serverlist || !out) { pg_set_error("pgx_boot_selftest: NULL argument"); return -1; }
+  struct pg pg;
+  memset(&pg, 0, sizeof(pg));
+  if (pg_parse_hosts(serverlist, &pg.hosts, &pg.world_size)) return -1;
+  int rc = -1, *fds = NULL;
+  if (rank < 0 || rank >= pg.world_size) { pg_set_error("pgx_boot_selftest: bad rank"); goto out; }
+  pg.rank = rank;
+  pg.port = port;
+  if (pg_boot_open(&pg, &fds)) goto out;
+  if (pg_boot_allgather(&pg, fds, &value, out, sizeof(int)) == 0 && pg_boot_barrier(&pg, fds) == 0) rc = 0;
+out:
+  pg_boot_close(fds, pg.world_size);
+  for (int i = 0; i < pg.world_size; ++i) free(pg.hosts[i]);
+  free(pg.hosts);
+  return rc;
+}

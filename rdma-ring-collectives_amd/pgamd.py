@@ -86,6 +86,7 @@ _SIGS = {
     "pg_get_stats": (_I, [_VP, ctypes.POINTER(PgStats)]),
     "pgx_reduce_host": (_I, [_VP, _CVP, _SZ, _I, _I, _SZ]),
     "pg_last_error": (ctypes.c_char_p, []),
+    "pgx_boot_selftest": (_I, [ctypes.c_char_p, _I, _I, _I, ctypes.POINTER(_I)]),
     # include/pgk.h
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
