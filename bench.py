@@ -215,6 +215,53 @@ def host_leg(lib, reps=3):
     return out
 
 
+def config1_leg(lib):
+    """BASELINE config 1 (2-rank ring, int32 sum, count 1,048,576): each rank
+    reduces one 2 MiB block (524,288 elements).  CPU: the reference's own
+    pg_reduce_scatter(W=2, R=0, chunk 2 MiB), which is exactly that one
+    reduce_inplace.  GPU: pgk_reduce on the same block, kernel
+    time and host-call wall time."""
+    import statistics
+    from oracle.pyoracle import Oracle, Reference
+    n = 1 << 19
+    out = {"block_bytes": n * 4}
+    orc = Oracle()
+    send = orc.fill(2 * n, pgamd.DT_INT32, 0, 11)
+    recv = orc.fill(2 * n, pgamd.DT_INT32, 0, 12)
+    try:
+        ref = Reference()
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            ref.lib.ref_reduce_scatter(0, 2, n * 4, send.ctypes.data, recv.ctypes.data, 2 * n, 0, 0)
+            ts.append(time.perf_counter() - t0)
+        out["cpu_reference_us"] = round(statistics.median(ts) * 1e6, 2)
+    except RuntimeError:
+        out["cpu_reference_us"] = None
+    d = torch.from_numpy(recv[n:]).cuda()
+    s_ = torch.from_numpy(send[:n]).cuda()
+    sh = torch.cuda.current_stream().cuda_stream
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    lib.pgk_event_create(ctypes.byref(a))
+    lib.pgk_event_create(ctypes.byref(b))
+    kt, wt = [], []
+    for _ in range(200):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pgamd.check(lib.pgk_reduce_timed(d.data_ptr(), s_.data_ptr(), n, pgamd.DT_INT32, 0, sh, a, b), "cfg1")
+        torch.cuda.synchronize()
+        wt.append(time.perf_counter() - t0)
+        ms = ctypes.c_float()
+        lib.pgk_event_elapsed_ms(a, b, ctypes.byref(ms))
+        kt.append(ms.value * 1e3)
+    lib.pgk_event_destroy(a)
+    lib.pgk_event_destroy(b)
+    out["gpu_kernel_us"] = round(statistics.median(kt), 2)
+    out["gpu_call_wall_us"] = round(statistics.median(wt) * 1e6, 2)
+    out["note"] = "2 MiB is launch/latency-bound on the GPU (6 MiB of traffic = 1 us at HBM rate)"
+    return out
+
+
 def load_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC pass (see
     profiles/README.md): (FETCH_SIZE*2 + WRITE_SIZE) KiB per dispatch, gfx950
@@ -374,6 +421,12 @@ def main():
             host = host_leg(lib)
         except Exception as e:
             host = {"error": f"{type(e).__name__}: {e}"}
+    cfg1 = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        try:
+            cfg1 = config1_leg(lib)
+        except Exception as e:
+            cfg1 = {"error": f"{type(e).__name__}: {e}"}
 
     line = None
     if rank == 0:
@@ -397,6 +450,7 @@ def main():
                          "bytes_per_launch": bytes_per_step},
             "cpu_baseline": cpu,
             "host_staged": host,
+            "config1": cfg1,
             "ring": None,
             "kernel": lib.pgk_version().decode(),
         }
