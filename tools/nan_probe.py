@@ -1,5 +1,5 @@
 import sys, numpy as np, torch
-sys.path[:0]=['/root/repo','/root/repo/rdma-ring-collectives_amd']
+import pathlib; R=pathlib.Path(__file__).resolve().parents[1]; sys.path[:0]=[str(R), str(R/'rdma-ring-collectives_amd')]
 import pgamd
 lib=pgamd.load()
 a=np.array([np.inf, 0.0, np.nan, -np.nan, np.inf, 1e308], np.float64)
