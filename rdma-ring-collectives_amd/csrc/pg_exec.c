@@ -88,17 +88,32 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
       hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
       PG_CHECK_HIP(hipEventRecord(rev, im->comm));
       PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-      for (int s = i; s < j; ++s) {
-        if (!st[s].red_elems) continue;
+      /* one launch per run of segments that are contiguous in both operands
+       * (a batch's segments are neighbours in the same block) */
+      const int64_t es = pg_elem_size(dt);
+      int s = i;
+      while (s < j) {
+        if (!st[s].red_elems) { ++s; continue; }
+        int e = s + 1;
+        int64_t elems = st[s].red_elems;
+        while (e < j && st[e].red_elems && st[e].red_dst_buf == st[s].red_dst_buf &&
+               st[e].red_src_buf == st[s].red_src_buf &&
+               st[e].red_dst_off == st[s].red_dst_off + elems * es &&
+               st[e].red_src_off == st[s].red_src_off + elems * es) {
+          elems += st[e].red_elems;
+          ++e;
+        }
         if (pgk_reduce(at(bufs, st[s].red_dst_buf, st[s].red_dst_off),
                        at(bufs, st[s].red_src_buf, st[s].red_src_off),
-                       (size_t)st[s].red_elems, dt, op, (void *)im->red)) {
+                       (size_t)elems, dt, op, (void *)im->red)) {
           pg_set_error("pg_exec: %s", pgk_last_error());
           return -1;
         }
-        PG_CHECK_HIP(hipEventRecord(im->red_ev[st[s].seg], im->red));
         im->stats.reduce_launches += 1;
-        im->stats.reduce_elems += st[s].red_elems;
+        im->stats.reduce_elems += elems;
+        for (int t = s; t < e; ++t)
+          if (st[t].red_elems) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[t].seg], im->red));
+        s = e;
       }
     }
     ++nb;
