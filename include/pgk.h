@@ -54,6 +54,17 @@ PG_API int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int
 PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                      void *stream);
 
+/* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
+ * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]
+ * (k = nsrc; requires ceil(n / block_elems) <= k): block b folded in exactly
+ * the order the ring reduce-scatter uses for it. */
+PG_API int pgk_fold_blocks(void *out, const void *const *srcs, int nsrc, size_t n, size_t block_elems,
+                           int dt, int op, void *stream);
+
+/* Copy k <= 16 byte ranges srcs[j] -> dsts[j] (bytes[j] each, 4-byte aligned,
+ * sources may be peer memory) in one launch. */
+PG_API int pgk_gather(void *const *dsts, const void *const *srcs, const size_t *bytes, int k, void *stream);
+
 /* Device helpers for hosts that do not link HIP themselves (ctypes, cgo ...). */
 PG_API int pgk_device_count(int *count);
 PG_API int pgk_set_device(int device);

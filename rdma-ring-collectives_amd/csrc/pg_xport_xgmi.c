@@ -32,7 +32,7 @@ struct xgmi_ctx {
   void *mem;                    /* my allocation: XG_SLOTS * cap bytes      */
   size_t cap;                   /* bytes per slot                           */
   void **peer;                  /* peer[q] = rank q's allocation, mapped    */
-  hipStream_t *cs;              /* one copy stream per source rank          */
+  size_t oneshot_max;           /* all-reduce at most this many bytes: one-shot */
   unsigned long gen;            /* collective calls so far (slot parity)    */
 };
 
@@ -92,10 +92,10 @@ int pg_xport_xgmi_init(struct pg *pg) {
   if (!x) return -1;
   im->xctx = x;
   x->peer = (void **)calloc((size_t)pg->world_size, sizeof(void *));
-  x->cs = (hipStream_t *)calloc((size_t)pg->world_size, sizeof(hipStream_t));
-  if (!x->peer || !x->cs) { pg_set_error("xgmi: out of host memory"); return -1; }
-  for (int q = 0; q < pg->world_size; ++q)
-    PG_CHECK_HIP(hipStreamCreateWithFlags(&x->cs[q], hipStreamNonBlocking));
+  if (!x->peer) { pg_set_error("xgmi: out of host memory"); return -1; }
+  x->oneshot_max = 1u << 20;
+  const char *e = getenv("PG_ONESHOT_MAX");
+  if (e && *e) x->oneshot_max = (size_t)strtoull(e, NULL, 0);
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
   return pg_boot_barrier(pg, im->boot_fds);
 }
@@ -107,9 +107,6 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   /* peers may still be reading my last contribution: meet them first */
   if (x->mem && im->boot_fds) pg_boot_barrier(pg, im->boot_fds);
   unmap(pg, x);
-  if (x->cs)
-    for (int q = 0; q < pg->world_size; ++q) if (x->cs[q]) hipStreamDestroy(x->cs[q]);
-  free(x->cs);
   free(x->peer);
   free(x);
   im->xctx = NULL;
@@ -182,20 +179,28 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   return 0;
 }
 
-/* Gather: copy block q (elements [off(q), off(q)+len(q)) of slot `which` of
- * rank q) into full + off(q), all ranks' copies concurrently. */
+/* Gather: block q (elements [off(q), off(q)+len(q)) of slot `which` of rank
+ * q) into full + off(q), every rank's range in one launch (pgk_gather). */
 static int gather(struct pg *pg, char *full, int which, int count, int uniform, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt);
+  void *dst[16];
+  const void *src[16];
+  size_t bytes[16];
+  int k = 0;
   for (int q = 0; q < pg->world_size; ++q) {
     size_t off, len;
     if (uniform) { off = (size_t)q * (size_t)count; len = (size_t)count; }
     else pg_block_range(count, pg->world_size, q, &off, &len);
     if (!len) continue;
-    const char *src = slot(x, q, which) + (uniform ? 0 : off * es);
-    PG_CHECK_HIP(hipMemcpyAsync(full + off * es, src, len * es, hipMemcpyDeviceToDevice, x->cs[q]));
+    dst[k] = full + off * es;
+    src[k] = slot(x, q, which) + (uniform ? 0 : off * es);
+    bytes[k] = len * es;
+    ++k;
   }
-  for (int q = 0; q < pg->world_size; ++q) PG_CHECK_HIP(hipStreamSynchronize(x->cs[q]));
+  if (pgk_gather(dst, src, bytes, k, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
   return 0;
 }
 
@@ -229,6 +234,26 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   int rd = is_dev(recvbuf), which = (int)(x->gen & 1);
   char *xs;
   if (publish(pg, sendbuf, bytes, is_dev(sendbuf), &xs)) return -1;
+  if (bytes <= x->oneshot_max) {
+    /* small message: every rank folds the whole vector itself, each block in
+     * its ring order -- one launch, no second barrier */
+    char *full = (char *)recvbuf;
+    if (!rd) {
+      if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
+      full = (char *)im->dout;
+    }
+    const void *srcs[16];
+    for (int q = 0; q < pg->world_size; ++q) srcs[q] = slot(x, q, which);
+    size_t blk = ((size_t)count + (size_t)pg->world_size - 1) / (size_t)pg->world_size;
+    if (count && pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, dt, op, (void *)im->red)) {
+      pg_set_error("xgmi: %s", pgk_last_error());
+      return -1;
+    }
+    PG_CHECK_HIP(hipStreamSynchronize(im->red));
+    if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
+    x->gen++;
+    return 0;
+  }
   PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
   /* my block of the result goes to R[which] so that every rank can gather it */
   if (fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, which, off, len, dt, op)) return -1;

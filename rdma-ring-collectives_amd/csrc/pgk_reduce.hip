@@ -167,6 +167,54 @@ __global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_scalar(T* __restri
   }
 }
 
+// One-shot all-reduce fold: element i belongs to ring block b = i / block_elems
+// and is folded in that block's ring order, src[(b+1)%k] op src[(b+2)%k] ...
+// op src[b] -- the order the reduce-scatter uses for block b, so every rank
+// computing the whole vector this way gets the all-reduce result bit for bit.
+// Used for small messages, where one launch beats reduce-scatter + gather.
+template <typename T, int OP>
+__global__ __launch_bounds__(kMultiBlock) void k_fold_blocks(T* __restrict__ out, SrcList<T> src, int k,
+                                                             size_t n, size_t block_elems) {
+  const size_t stride = (size_t)gridDim.x * kMultiBlock;
+  for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < n; i += stride) {
+    int b = (int)(i / block_elems);
+    int q = b + 1 >= k ? b + 1 - k : b + 1;
+    T acc = src.p[q][i];
+    for (int j = 1; j < k; ++j) {
+      q = q + 1 == k ? 0 : q + 1;
+      acc = apply<OP>(acc, src.p[q][i]);
+    }
+    out[i] = acc;
+  }
+}
+
+// Gather: copy up to 16 byte ranges (one per source rank, possibly peer
+// memory over xGMI) in one launch; blockIdx.y picks the range.  16-byte
+// vectors when a range is 16-B aligned at both ends, else 4-byte words.
+struct CopyList {
+  const char* src[kMaxSrc];
+  char* dst[kMaxSrc];
+  size_t bytes[kMaxSrc];
+};
+
+__global__ __launch_bounds__(kMultiBlock) void k_gather(CopyList cl) {
+  const int r = blockIdx.y;
+  const char* s = cl.src[r];
+  char* d = cl.dst[r];
+  const size_t nb = cl.bytes[r];
+  const size_t stride = (size_t)gridDim.x * kMultiBlock;
+  size_t t = (size_t)blockIdx.x * kMultiBlock + threadIdx.x;
+  if ((((uintptr_t)s | (uintptr_t)d | nb) & 15) == 0) {
+    const u32x4* vs = reinterpret_cast<const u32x4*>(s);
+    u32x4* vd = reinterpret_cast<u32x4*>(d);
+    for (size_t i = t; i < nb / 16; i += stride) st<true>(vd + i, ld<true>(vs + i));
+  } else {
+    const uint32_t* ws = reinterpret_cast<const uint32_t*>(s);
+    uint32_t* wd = reinterpret_cast<uint32_t*>(d);
+    for (size_t i = t; i < nb / 4; i += stride) wd[i] = ws[i];
+  }
+}
+
 // ---- host side ---------------------------------------------------------------
 
 thread_local char g_err[256] = "";
@@ -364,6 +412,70 @@ int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int
   return 0;
 }
 
+
+int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size_t block_elems, int dt, int op,
+                    void* stream) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
+  if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
+  if (n == 0) return 0;
+  if (!out || !srcs || block_elems == 0 || (n + block_elems - 1) / block_elems > (size_t)nsrc) {
+    set_err("pgk: bad fold_blocks arguments");
+    return -1;
+  }
+  size_t g = (n + kMultiBlock - 1) / kMultiBlock;
+  if (g > 65536) g = 65536;
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == PGK_DT_INT32) {
+    SrcList<uint32_t> sl{};
+    for (int j = 0; j < nsrc; ++j) sl.p[j] = (const uint32_t*)srcs[j];
+    if (op == PGK_OP_SUM)
+      hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
+                         (uint32_t*)out, sl, nsrc, n, block_elems);
+    else
+      hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
+                         (uint32_t*)out, sl, nsrc, n, block_elems);
+  } else {
+    SrcList<double> sl{};
+    for (int j = 0; j < nsrc; ++j) sl.p[j] = (const double*)srcs[j];
+    if (op == PGK_OP_SUM)
+      hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
+                         (double*)out, sl, nsrc, n, block_elems);
+    else
+      hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
+                         (double*)out, sl, nsrc, n, block_elems);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_gather(void* const* dsts, const void* const* srcs, const size_t* bytes, int k, void* stream) {
+  if (k < 0 || k > kMaxSrc || (k && (!dsts || !srcs || !bytes))) { set_err("pgk: bad gather arguments"); return -1; }
+  CopyList cl{};
+  size_t most = 0;
+  int m = 0;
+  for (int j = 0; j < k; ++j) {
+    if (!bytes[j]) continue;
+    if ((bytes[j] & 3) || (((uintptr_t)dsts[j] | (uintptr_t)srcs[j]) & 3)) {
+      set_err("pgk: gather ranges must be 4-byte aligned");
+      return -1;
+    }
+    cl.src[m] = (const char*)srcs[j];
+    cl.dst[m] = (char*)dsts[j];
+    cl.bytes[m] = bytes[j];
+    if (bytes[j] > most) most = bytes[j];
+    ++m;
+  }
+  if (!m) return 0;
+  size_t g = (most / 16 + kMultiBlock - 1) / kMultiBlock;
+  if (g == 0) g = 1;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)g, (unsigned)m), dim3(kMultiBlock), 0, (hipStream_t)stream, cl);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
 
 int pgk_reduce(void* dst, const void* src, size_t n, int dt, int op, void* stream) {
   return launch(dst, dst, src, n, dt, op, stream);

@@ -91,6 +91,8 @@ _SIGS = {
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
+    "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _VP]),
+    "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),
     "pgk_device_count": (_I, [ctypes.POINTER(_I)]),
     "pgk_set_device": (_I, [_I]),
     "pgk_synchronize": (_I, []),

@@ -188,3 +188,34 @@ def test_reduce_multi_fold_order(gpu, lib, oracle, dt, op):
     srcs = (ctypes.c_void_p * 17)()
     assert lib.pgk_reduce_multi(ptr(out), srcs, 17, 4, dt, op, stream(torch)) == -1
     assert lib.pgk_reduce_multi(ptr(out), srcs, 0, 4, dt, op, stream(torch)) == -1
+
+
+def test_fold_blocks_and_gather(gpu, lib, oracle):
+    """pgk_fold_blocks == the oracle's ring all-reduce (each block in its ring
+    order); pgk_gather copies every range, 16-B and 4-B aligned forms."""
+    import ctypes
+    torch = gpu
+    for world, count, dt, op in ((2, 1001, 1, 0), (3, 10, 0, 1), (8, 65541, 1, 1), (5, 4, 1, 0), (4, 4099, 0, 0)):
+        xs = [oracle.fill(count, dt, op, 77 + r) for r in range(world)]
+        want = oracle.ring_all_reduce(xs, dt, op)[0]
+        D = [to_dev(torch, x) for x in xs]
+        out = torch.zeros(count, dtype=D[0].dtype, device="cuda")
+        srcs = (ctypes.c_void_p * world)(*[ptr(d) for d in D])
+        blk = -(-count // world)
+        assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, dt, op, stream(torch)) == 0
+        assert to_host(torch, out).tobytes() == want.tobytes(), (world, count, dt, op)
+    # gather: ranges of different sizes/alignments into one buffer
+    src = torch.arange(1 << 16, dtype=torch.int32, device="cuda")
+    dst = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    pieces = [(0, 0, 4096), (4096, 8192, 3), (5000, 20000, 1027), (30000, 40000, 8192)]   # (src elem, dst elem, n)
+    ds = (ctypes.c_void_p * 4)(*[ptr(dst) + d * 4 for _, d, _ in pieces])
+    ss = (ctypes.c_void_p * 4)(*[ptr(src) + s_ * 4 for s_, _, _ in pieces])
+    nb = (ctypes.c_size_t * 4)(*[n * 4 for _, _, n in pieces])
+    assert lib.pgk_gather(ds, ss, nb, 4, stream(torch)) == 0
+    got = to_host(torch, dst)
+    want = np.zeros(1 << 16, np.int32)
+    for s_, d, n in pieces:
+        want[d:d + n] = np.arange(s_, s_ + n)
+    assert np.array_equal(got, want)
+    bad = (ctypes.c_size_t * 1)(3)
+    assert lib.pgk_gather(ds, ss, bad, 1, stream(torch)) == -1

@@ -19,7 +19,8 @@ CASES = [  # coll, dt, op, count, on_dev, in_place
     ("rs", 0, 0, 0, True, False), ("rs", 1, 0, (1 << 20) + 3, True, False),
     ("ag", 1, 0, 257, True, False), ("ag", 0, 0, 64, False, False), ("ag", 1, 0, 33, True, True),
     ("ar", 1, 0, 100003, True, False), ("ar", 0, 1, 999, False, False), ("ar", 1, 1, 4096, True, True),
-    ("ar", 0, 0, 7, False, True), ("rs", 1, 0, 5000, True, False),
+    ("ar", 0, 0, 7, False, True), ("rs", 1, 0, 5000, True, False), ("ar", 1, 0, 300001, True, False),
+    ("ar", 0, 1, 524288, False, True),
 ]
 
 
@@ -31,9 +32,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, oneshot_max):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000")
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max))
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -93,13 +94,16 @@ def _worker(rank, world, port, q):
     q.put((rank, fails))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_xgmi_multiprocess(gpu, world):
+@pytest.mark.parametrize("world,oneshot_max", [(2, 1 << 20), (3, 1 << 20), (4, 1 << 20), (8, 1 << 20),
+                                               (2, 0), (5, 0), (4, 1 << 40)])
+def test_xgmi_multiprocess(gpu, world, oneshot_max):
+    """oneshot_max selects the all-reduce form: 0 = always reduce-scatter +
+    gather, 2^40 = always the one-shot fold, 1 MiB = the default split."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
