@@ -282,6 +282,88 @@ int pg_boot_barrier(struct pg *pg, const int *fds) {
   return rc;
 }
 
+/* ---- node-local barrier over POSIX shared memory --------------------------------
+ * For transports whose ranks are by construction on one node (xgmi needs HIP
+ * IPC), a barrier on a shared page costs a few microseconds instead of two TCP
+ * hops through rank 0 with their scheduling jitter.  Sense-reversing counter;
+ * every wait is bounded (PG_BARRIER_TIMEOUT_MS, default 300 s) so a dead peer
+ * turns into an error, never a hang. */
+#include <fcntl.h>
+#include <sched.h>
+#include <stdatomic.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+
+struct pg_shm_bar {
+  _Atomic unsigned count;
+  _Atomic unsigned gen;
+};
+
+int pg_shm_open(struct pg *pg, const int *fds, void **bar_out) {
+  char name[64], all[64 * 64];
+  memset(name, 0, sizeof(name));
+  if (pg->world_size > 64) return -1;
+  if (pg->rank == 0) {
+    snprintf(name, sizeof(name), "/pgamd.%d.%d.%ld", (int)getpid(), pg->port, (long)now_ms());
+    int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, 4096)) {
+      if (fd >= 0) close(fd);
+      name[0] = 0;                              /* tell the others: no shm barrier */
+    } else {
+      close(fd);
+    }
+  }
+  if (pg_boot_allgather(pg, fds, name, all, sizeof(name))) return -1;
+  memcpy(name, all, sizeof(name));             /* rank 0's name */
+  void *p = NULL;
+  int ok = 0;
+  if (name[0]) {
+    int fd = shm_open(name, O_RDWR, 0600);
+    if (fd >= 0) {
+      p = mmap(NULL, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+      if (p == MAP_FAILED) p = NULL;
+    }
+    ok = p != NULL;
+  }
+  /* everyone mapped (or gave up) before rank 0 unlinks the name */
+  char okc = (char)ok, oks[64];
+  int rc = pg_boot_allgather(pg, fds, &okc, oks, 1);
+  if (pg->rank == 0 && name[0]) shm_unlink(name);
+  if (rc) { if (p) munmap(p, 4096); return -1; }
+  for (int q = 0; q < pg->world_size; ++q)
+    if (!oks[q]) { if (p) munmap(p, 4096); *bar_out = NULL; return 0; }   /* fall back to TCP */
+  *bar_out = p;
+  return 0;
+}
+
+void pg_shm_close(void *bar) {
+  if (bar) munmap(bar, 4096);
+}
+
+int pg_shm_barrier(struct pg *pg, void *barp) {
+  struct pg_shm_bar *b = (struct pg_shm_bar *)barp;
+  int timeout_ms = 300000;
+  env_int("PG_BARRIER_TIMEOUT_MS", &timeout_ms);
+  unsigned g = atomic_load_explicit(&b->gen, memory_order_acquire);
+  if (atomic_fetch_add_explicit(&b->count, 1, memory_order_acq_rel) == (unsigned)pg->world_size - 1) {
+    atomic_store_explicit(&b->count, 0, memory_order_relaxed);
+    atomic_store_explicit(&b->gen, g + 1, memory_order_release);
+    return 0;
+  }
+  long deadline = 0;
+  for (unsigned long spin = 0;; ++spin) {
+    if (atomic_load_explicit(&b->gen, memory_order_acquire) != g) return 0;
+    if (spin < 4096) { __builtin_ia32_pause(); continue; }
+    if (!deadline) deadline = now_ms() + timeout_ms;
+    if ((spin & 255) == 0 && now_ms() > deadline) {
+      pg_set_error("barrier: peers did not arrive within %d ms", timeout_ms);
+      return -1;
+    }
+    sched_yield();
+  }
+}
+
 /* Test hook (include/pg_ext.h): the bootstrap star without any GPU. */
 int pgx_boot_selftest(const char *serverlist, int rank, int port, int value, int *out) {
   if (!serverlist || !out) { pg_set_error("pgx_boot_selftest: NULL argument"); return -1; }
@@ -293,10 +375,18 @@ int pgx_boot_selftest(const char *serverlist, int rank, int port, int value, int
   pg.rank = rank;
   pg.port = port;
   if (pg_boot_open(&pg, &fds)) goto out;
-  if (pg_boot_allgather(&pg, fds, &value, out, sizeof(int)) == 0 && pg_boot_barrier(&pg, fds) == 0) rc = 0;
+  if (pg_boot_allgather(&pg, fds, &value, out, sizeof(int)) == 0 && pg_boot_barrier(&pg, fds) == 0) {
+    void *bar = NULL;                            /* and the node-local shm barrier */
+    if (pg_shm_open(&pg, fds, &bar) == 0 && bar) {
+      rc = 0;
+      for (int i = 0; i < 1000 && rc == 0; ++i) rc = pg_shm_barrier(&pg, bar);
+      pg_shm_close(bar);
+    }
+  }
 out:
   pg_boot_close(fds, pg.world_size);
   for (int i = 0; i < pg.world_size; ++i) free(pg.hosts[i]);
   free(pg.hosts);
   return rc;
 }
+

@@ -101,6 +101,9 @@ int pg_boot_open(struct pg *pg, int **fds_out);
 void pg_boot_close(int *fds, int n);
 int pg_boot_allgather(struct pg *pg, const int *fds, const void *mine, void *all, size_t bytes);
 int pg_boot_barrier(struct pg *pg, const int *fds);
+int pg_shm_open(struct pg *pg, const int *fds, void **bar_out);   /* NULL bar: fall back to TCP */
+void pg_shm_close(void *bar);
+int pg_shm_barrier(struct pg *pg, void *bar);
 
 #define PG_CHECK_HIP(expr)                                                          \
   do {                                                                              \

@@ -33,11 +33,19 @@ struct xgmi_ctx {
   size_t cap;                   /* bytes per slot                           */
   void **peer;                  /* peer[q] = rank q's allocation, mapped    */
   size_t oneshot_max;           /* all-reduce at most this many bytes: one-shot */
+  void *bar;                    /* node-local shm barrier (pg_boot.c), or NULL */
   unsigned long gen;            /* collective calls so far (slot parity)    */
 };
 
 static struct xgmi_ctx *ctx_of(struct pg *pg) {
   return (struct xgmi_ctx *)((struct pg_impl *)pg->impl)->xctx;
+}
+
+/* All ranks of this transport share one node: shm barrier, TCP as fallback. */
+static int barrier(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = (struct xgmi_ctx *)im->xctx;
+  return x->bar ? pg_shm_barrier(pg, x->bar) : pg_boot_barrier(pg, im->boot_fds);
 }
 
 static char *slot(struct xgmi_ctx *x, int q, int which) {
@@ -63,7 +71,7 @@ static int ensure(struct pg *pg, size_t bytes) {
   size_t cap = x->cap ? x->cap : XG_GRANULE;
   while (cap < bytes) cap *= 2;
   /* nobody may still read the old slots */
-  if (x->mem && pg_boot_barrier(pg, im->boot_fds)) return -1;
+  if (x->mem && barrier(pg)) return -1;
   unmap(pg, x);
   PG_CHECK_HIP(hipMalloc(&x->mem, cap * XG_SLOTS));
   x->cap = cap;
@@ -97,7 +105,9 @@ int pg_xport_xgmi_init(struct pg *pg) {
   const char *e = getenv("PG_ONESHOT_MAX");
   if (e && *e) x->oneshot_max = (size_t)strtoull(e, NULL, 0);
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
-  return pg_boot_barrier(pg, im->boot_fds);
+  const char *nb = getenv("PG_NO_SHM_BARRIER");
+  if (!(nb && *nb == '1') && pg_shm_open(pg, im->boot_fds, &x->bar)) return -1;
+  return barrier(pg);
 }
 
 void pg_xport_xgmi_destroy(struct pg *pg) {
@@ -105,8 +115,9 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   struct xgmi_ctx *x = ctx_of(pg);
   if (!x) return;
   /* peers may still be reading my last contribution: meet them first */
-  if (x->mem && im->boot_fds) pg_boot_barrier(pg, im->boot_fds);
+  if (x->mem && im->boot_fds) barrier(pg);
   unmap(pg, x);
+  pg_shm_close(x->bar);
   free(x->peer);
   free(x);
   im->xctx = NULL;
@@ -132,7 +143,7 @@ static int publish(struct pg *pg, const void *src, size_t bytes, int src_dev, ch
                                 im->red));
     PG_CHECK_HIP(hipStreamSynchronize(im->red));
   }
-  return pg_boot_barrier(pg, im->boot_fds);
+  return barrier(pg);
 }
 
 /* out = fold over ranks, in ring order, of block `b` of slot `which`. */
@@ -258,7 +269,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   /* my block of the result goes to R[which] so that every rank can gather it */
   if (fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, which, off, len, dt, op)) return -1;
   PG_CHECK_HIP(hipStreamSynchronize(im->red));
-  if (pg_boot_barrier(pg, im->boot_fds)) return -1;
+  if (barrier(pg)) return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;

@@ -1,4 +1,5 @@
-"""The TCP bootstrap star (pg_boot.c) across real processes, no GPU: rank 0
+"""The TCP bootstrap star (pg_boot.c) and the node-local shm barrier across
+real processes, no GPU: rank 0
 relays every rank's value to all (the path that carries the RCCL unique id
 and the xgmi IPC handles), late joiners are retried, and a rank outside the
 list is rejected."""
