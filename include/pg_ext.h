@@ -110,6 +110,11 @@ struct pg_stats {
   int64_t reduce_launches;
   int64_t reduce_elems;  /* elements reduced by this rank                   */
   int64_t bytes_sent, bytes_recv;
+  /* host-side phase times of the last call (xgmi transport) */
+  double sync_us;        /* waiting for the caller's pending GPU work       */
+  double copy_us;        /* input -> exchange slot (H2D or D2D), synced     */
+  double barrier_us;     /* meeting the other ranks                         */
+  double kernel_us;      /* fold / gather launch + completion               */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

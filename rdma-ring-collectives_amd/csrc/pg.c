@@ -48,6 +48,31 @@ static double now_us(void) {
   return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
 }
 
+/* Wait for `s` to drain: poll hipStreamQuery for up to PG_SPIN_US (default
+ * 200 us) -- a short collective finishes well inside that, without the wake-up
+ * latency of a blocking wait -- then fall back to hipStreamSynchronize.  No
+ * process-wide scheduling flags are touched. */
+int pg_stream_wait(hipStream_t s) {
+  static double spin_us = -1.0;
+  if (spin_us < 0) {
+    const char *e = getenv("PG_SPIN_US");
+    spin_us = (e && *e) ? atof(e) : 200.0;
+  }
+  double t0 = spin_us > 0 ? now_us() : 0;
+  while (spin_us > 0) {
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) {
+      pg_set_error("stream wait: %s", hipGetErrorString(e));
+      return -1;
+    }
+    if (now_us() - t0 > spin_us) break;
+    __builtin_ia32_pause();
+  }
+  PG_CHECK_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
 int pg_ensure(void **buf, size_t *cap, size_t bytes) {
   if (bytes <= *cap && (*buf || bytes == 0)) return 0;
   if (*buf) { hipFree(*buf); *buf = NULL; *cap = 0; }
@@ -208,8 +233,7 @@ int pg_get_stats(void *pg_handle, struct pg_stats *out) {
 static void stats_begin(struct pg_impl *im) { memset(&im->stats, 0, sizeof(im->stats)); }
 
 static int sync_ring(struct pg_impl *im, int timed) {
-  PG_CHECK_HIP(hipStreamSynchronize(im->comm));
-  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
   if (timed) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;

@@ -19,9 +19,11 @@
  * per call enough: a slot is rewritten two calls later, and every rank passed
  * the intervening call's barrier only after finishing its reads.
  */
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "pg_impl.h"
 
@@ -41,6 +43,16 @@ static struct xgmi_ctx *ctx_of(struct pg *pg) {
   return (struct xgmi_ctx *)((struct pg_impl *)pg->impl)->xctx;
 }
 
+static double us_now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
+}
+
+static char *slot(struct xgmi_ctx *x, int q, int which) {
+  return (char *)x->peer[q] + (size_t)which * x->cap;
+}
+
 /* All ranks of this transport share one node: shm barrier, TCP as fallback. */
 static int barrier(struct pg *pg) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
@@ -48,40 +60,58 @@ static int barrier(struct pg *pg) {
   return x->bar ? pg_shm_barrier(pg, x->bar) : pg_boot_barrier(pg, im->boot_fds);
 }
 
-static char *slot(struct xgmi_ctx *x, int q, int which) {
-  return (char *)x->peer[q] + (size_t)which * x->cap;
-}
-
-static void unmap(struct pg *pg, struct xgmi_ctx *x) {
+static void unmap_peers(struct pg *pg, struct xgmi_ctx *x) {
   if (!x->peer) return;
   for (int q = 0; q < pg->world_size; ++q)
     if (q != pg->rank && x->peer[q]) hipIpcCloseMemHandle(x->peer[q]);
   memset(x->peer, 0, sizeof(void *) * (size_t)pg->world_size);
+}
+
+static void unmap(struct pg *pg, struct xgmi_ctx *x) {
+  unmap_peers(pg, x);
   if (x->mem) hipFree(x->mem);
   x->mem = NULL;
   x->cap = 0;
 }
 
 /* Collective: every rank calls with the same `bytes` (same count), so every
- * rank grows in the same call to the same size. */
+ * rank grows in the same call to the same size.
+ *
+ * Growth order matters (observed on ROCm 7.2, tests/test_xgmi_gpu.py::
+ * test_xgmi_slot_growth): unmapping the peers' old slots, then allocating and
+ * exporting the replacement failed with hipIpcGetMemHandle: invalid argument.
+ * So the replacement is allocated and exported while every old import is
+ * still mapped, and the old allocation is freed only after all ranks have
+ * dropped their mappings of it. */
 static int ensure(struct pg *pg, size_t bytes) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
   if (bytes <= x->cap && x->mem) return 0;
   size_t cap = x->cap ? x->cap : XG_GRANULE;
   while (cap < bytes) cap *= 2;
-  /* nobody may still read the old slots */
-  if (x->mem && barrier(pg)) return -1;
-  unmap(pg, x);
-  PG_CHECK_HIP(hipMalloc(&x->mem, cap * XG_SLOTS));
-  x->cap = cap;
+  if (x->mem && barrier(pg)) return -1;      /* nobody still reads the old slots */
+  void *fresh = NULL;
+  PG_CHECK_HIP(hipMalloc(&fresh, cap * XG_SLOTS));
   hipIpcMemHandle_t mine, *all = (hipIpcMemHandle_t *)malloc(sizeof(hipIpcMemHandle_t) * (size_t)pg->world_size);
-  if (!all) { pg_set_error("xgmi: out of host memory"); return -1; }
-  hipError_t e = hipIpcGetMemHandle(&mine, x->mem);
-  if (e != hipSuccess) { free(all); pg_set_error("xgmi: hipIpcGetMemHandle: %s", hipGetErrorString(e)); return -1; }
+  if (!all) { hipFree(fresh); pg_set_error("xgmi: out of host memory"); return -1; }
+  hipError_t e = hipIpcGetMemHandle(&mine, fresh);
+  if (e != hipSuccess) {
+    free(all);
+    hipFree(fresh);
+    pg_set_error("xgmi: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    return -1;
+  }
+  if (x->mem) {
+    unmap_peers(pg, x);
+    if (barrier(pg)) { free(all); hipFree(fresh); return -1; }   /* nobody maps my old slots */
+    hipFree(x->mem);
+  }
+  x->mem = fresh;
+  x->cap = cap;
+  x->peer[pg->rank] = x->mem;
   if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) { free(all); return -1; }
   for (int q = 0; q < pg->world_size; ++q) {
-    if (q == pg->rank) { x->peer[q] = x->mem; continue; }
+    if (q == pg->rank) continue;
     e = hipIpcOpenMemHandle(&x->peer[q], all[q], hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
       free(all);
@@ -137,13 +167,29 @@ static int publish(struct pg *pg, const void *src, size_t bytes, int src_dev, ch
   struct xgmi_ctx *x = ctx_of(pg);
   int which = (int)(x->gen & 1);
   *xslot = slot(x, pg->rank, which);
+  double t0 = us_now();
   if (src_dev) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  double t1 = us_now();
   if (bytes) {
-    PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                im->red));
-    PG_CHECK_HIP(hipStreamSynchronize(im->red));
+    if (src_dev && ((uintptr_t)src & 3) == 0 && (bytes & 3) == 0) {
+      /* device input: a copy kernel (the DMA engine path costs ~50 us to
+       * start for a small copy) */
+      void *d[1] = {*xslot};
+      const void *sv[1] = {src};
+      size_t nb[1] = {bytes};
+      if (pgk_gather(d, sv, nb, 1, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
+    } else {
+      PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                  im->red));
+    }
+    if (pg_stream_wait(im->red)) return -1;
   }
-  return barrier(pg);
+  double t2 = us_now();
+  int rc = barrier(pg);
+  im->stats.sync_us += t1 - t0;
+  im->stats.copy_us += t2 - t1;
+  im->stats.barrier_us += us_now() - t2;
+  return rc;
 }
 
 /* out = fold over ranks, in ring order, of block `b` of slot `which`. */
@@ -179,12 +225,10 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
     if (pg_ensure(&im->dout, &im->dout_cap, len * es)) return -1;
     out = im->dout;
   }
-  PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
+  double tk = us_now();
   if (fold_block(pg, out, (int)(x->gen & 1), off, len, dt, op)) return -1;
-  PG_CHECK_HIP(hipEventRecord(im->t1, im->red));
-  PG_CHECK_HIP(hipStreamSynchronize(im->red));
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
+  if (pg_stream_wait(im->red)) return -1;
+  im->stats.kernel_us += us_now() - tk;
   if (!rd && len) PG_CHECK_HIP(hipMemcpy(recvbuf, out, len * es, hipMemcpyDeviceToHost));
   x->gen++;
   return 0;
@@ -211,7 +255,7 @@ static int gather(struct pg *pg, char *full, int which, int count, int uniform, 
     ++k;
   }
   if (pgk_gather(dst, src, bytes, k, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
-  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (pg_stream_wait(im->red)) return -1;
   return 0;
 }
 
@@ -256,30 +300,33 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     const void *srcs[16];
     for (int q = 0; q < pg->world_size; ++q) srcs[q] = slot(x, q, which);
     size_t blk = ((size_t)count + (size_t)pg->world_size - 1) / (size_t)pg->world_size;
+    double tk = us_now();
     if (count && pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, dt, op, (void *)im->red)) {
       pg_set_error("xgmi: %s", pgk_last_error());
       return -1;
     }
-    PG_CHECK_HIP(hipStreamSynchronize(im->red));
+    if (pg_stream_wait(im->red)) return -1;
+    im->stats.kernel_us += us_now() - tk;
     if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
     x->gen++;
     return 0;
   }
-  PG_CHECK_HIP(hipEventRecord(im->t0, im->red));
+  double tk = us_now();
   /* my block of the result goes to R[which] so that every rank can gather it */
   if (fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, which, off, len, dt, op)) return -1;
-  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  if (pg_stream_wait(im->red)) return -1;
+  double tb = us_now();
+  im->stats.kernel_us += tb - tk;
   if (barrier(pg)) return -1;
+  im->stats.barrier_us += us_now() - tb;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
     full = (char *)im->dout;
   }
+  double tg = us_now();
   if (gather(pg, full, 2 + which, count, 0, dt)) return -1;
-  PG_CHECK_HIP(hipEventRecord(im->t1, im->red));
-  PG_CHECK_HIP(hipStreamSynchronize(im->red));
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
+  im->stats.kernel_us += us_now() - tg;
   if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
   x->gen++;
   return 0;

@@ -53,6 +53,8 @@ class PgStats(ctypes.Structure):
         ("ring_us", ctypes.c_double),
         ("reduce_launches", ctypes.c_int64), ("reduce_elems", ctypes.c_int64),
         ("bytes_sent", ctypes.c_int64), ("bytes_recv", ctypes.c_int64),
+        ("sync_us", ctypes.c_double), ("copy_us", ctypes.c_double), ("barrier_us", ctypes.c_double),
+        ("kernel_us", ctypes.c_double),
     ]
 
 

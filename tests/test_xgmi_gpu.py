@@ -118,3 +118,64 @@ def test_xgmi_multiprocess(gpu, world, oneshot_max):
     for rank, fails in results:
         assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _grow_worker(rank, world, port, q):
+    """Exchange slots grow (64 MiB granule, doubling) inside a sequence of
+    calls; results checked against a closed form on the device."""
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port))
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        for count in (1 << 10, 9 << 20, 30 << 20, 1 << 12, 9 << 20):     # doubles: 8 KiB .. 240 MiB
+            i = torch.arange(count, device="cuda", dtype=torch.int64)
+            x = ((i % 1000) + rank).to(torch.float64)
+            want = ((i % 1000) * world + world * (world - 1) // 2).to(torch.float64)
+            y = torch.empty(count, dtype=torch.float64, device="cuda")
+            if lib.pg_all_reduce(x.data_ptr(), y.data_ptr(), count, 1, 0, h) != 0:
+                fails.append((count, pgamd.last_error()))
+                break
+            if not torch.equal(y, want):
+                fails.append((count, "mismatch"))
+            off, ln = pgamd.block_range(count, world, rank)
+            z = torch.empty(max(ln, 1), dtype=torch.float64, device="cuda")
+            if lib.pg_reduce_scatter(x.data_ptr(), z.data_ptr(), count, 1, 0, h) != 0 or \
+                    not torch.equal(z[:ln], want[off:off + ln]):
+                fails.append((count, "rs", pgamd.last_error()))
+            del i, x, y, z, want
+            torch.cuda.empty_cache()
+        lib.pg_close(h)
+    except Exception as e:
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_slot_growth(gpu, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grow_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=300))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)

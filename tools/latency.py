@@ -20,6 +20,13 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
 def worker(rank, world, port, q, sizes):
+    try:
+        _worker(rank, world, port, q, sizes)
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, [("error", repr(e))]))
+
+
+def _worker(rank, world, port, q, sizes):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port))
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     import ctypes
@@ -54,7 +61,11 @@ def worker(rank, world, port, q, sizes):
                     if i >= 3:
                         ts.append(time.perf_counter() - t0)
                 med = statistics.median(ts)
-                rows.append((nbytes, world - 1, 0, round(med * 1e6, 2), round(nbytes / med / 1e9, 3), coll, kind))
+                st = pgamd.stats(h)
+                phases = "sync %.0f copy %.0f barrier %.0f kernel %.0f wall %.0f" % (
+                    st["sync_us"], st["copy_us"], st["barrier_us"], st["kernel_us"], st["wall_us"])
+                rows.append((nbytes, world - 1, 0, round(med * 1e6, 2), round(nbytes / med / 1e9, 3), coll, kind,
+                             phases))
             del x, y
     lib.pg_close(h)
     q.put((rank, rows))
@@ -76,13 +87,13 @@ def main():
     ps = [ctx.Process(target=worker, args=(r, a.world, port, q, sizes)) for r in range(a.world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=600) for _ in range(a.world))
+    res = dict(q.get(timeout=300) for _ in range(a.world))
     for p in ps:
         p.join(timeout=60)
     out = pathlib.Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
     with out.open("w") as f:
-        f.write("size,rounds,inflight,time_us,GB/s,collective,memory\n")
+        f.write("size,rounds,inflight,time_us,GB/s,collective,memory,last_call_phases_us\n")
         for row in res[0]:
             f.write(",".join(map(str, row)) + "\n")
             print(*row)
