@@ -193,7 +193,8 @@ def cpu_baseline(args):
 
 def host_leg(lib, reps=3):
     """PCIe-inclusive rate of the same chunk reduce with dst/src in host memory
-    (pgx_reduce_host: 64 MiB pieces, two streams).  Reported, never `value`."""
+    (pgx_reduce_host: threaded H2D of both operands, reduce, threaded D2H).
+    Reported, never `value`."""
     out = {}
     n = N_ELEMS
     for kind in ("pageable", "pinned"):
@@ -201,17 +202,17 @@ def host_leg(lib, reps=3):
         s_ = torch.rand(n, dtype=torch.float64)
         if kind == "pinned":
             d, s_ = d.pin_memory(), s_.pin_memory()
-        pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 64 << 20), "host reduce")
+        pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 0), "host reduce")
         t0 = time.perf_counter()
         for _ in range(reps):
-            pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 64 << 20), "host reduce")
+            pgamd.check(lib.pgx_reduce_host(d.data_ptr(), s_.data_ptr(), n, DT, OP, 0), "host reduce")
         dt_ = (time.perf_counter() - t0) / reps
         out[kind] = {"ms": round(dt_ * 1e3, 3), "traffic_gibs": round(3 * n * 8 / dt_ / GIB, 2),
                      "payload_gibs": round(n * 8 / dt_ / GIB, 2),
                      "pcie_gbs": round(3 * n * 8 / dt_ / 1e9, 2)}
         del d, s_
-    out["note"] = ("256 MiB double sum, dst/src in host memory: H2D dst+src, reduce, D2H dst per "
-                   "64 MiB piece, 2 streams; pcie_gbs counts the 3*n*8 bytes that cross PCIe")
+    out["note"] = ("256 MiB double sum, dst/src in host memory: threaded H2D dst+src, reduce, threaded "
+                   "D2H dst (PG_COPY_THREADS, default 4); pcie_gbs counts the 3*n*8 bytes that cross PCIe")
     return out
 
 

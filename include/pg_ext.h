@@ -97,8 +97,8 @@ PG_API int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *
                 size_t eager_max, int inflight);
 
 /* The hot path with both operands in host memory: dst[i] = dst[i] op src[i]
- * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces on two
- * streams (copies of one piece overlap the reduce of the previous one).
+ * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces (0 =
+ * 256 MiB) with threaded host<->device copies (PG_COPY_THREADS).
  * Synchronous.  This is what the PCIe-inclusive rate in DESIGN.md measures. */
 PG_API int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
 

@@ -14,6 +14,7 @@
  * reference's `(op == OP_SUM) ? add : mul` does (src/pg.c:154,157).
  */
 #define _GNU_SOURCE
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -100,9 +101,67 @@ static int ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
   return na && nb && x < y + nb && y < x + na;
 }
 
+/* Host<->device copies of large buffers, optionally split over
+ * PG_COPY_THREADS threads (default 1: measured on MI355X + EPYC 9575F, one
+ * hipMemcpy of pageable memory already runs at the PCIe Gen5 x16 limit,
+ * ~53 GB/s, and 2/4/8 threads measured 52/51/49 GB/s; tools/copy_threads_probe.py).
+ * Kept for hosts whose single-thread staging is slower than the link. */
+struct copy_job {
+  void *dst;
+  const void *src;
+  size_t bytes;
+  int device;
+  hipError_t err;
+};
+
+static void *copy_thread(void *arg) {
+  struct copy_job *j = (struct copy_job *)arg;
+  j->err = hipSetDevice(j->device);
+  if (j->err == hipSuccess) j->err = hipMemcpy(j->dst, j->src, j->bytes, hipMemcpyDefault);
+  return NULL;
+}
+
+int pg_copy_parallel(void *dst, const void *src, size_t bytes) {
+  static int nthreads = -1;
+  if (nthreads < 0) {
+    const char *e = getenv("PG_COPY_THREADS");
+    nthreads = (e && *e) ? atoi(e) : 1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 16) nthreads = 16;
+  }
+  if (nthreads == 1 || bytes < (32u << 20)) {
+    PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return 0;
+  }
+  int dev = 0;
+  PG_CHECK_HIP(hipGetDevice(&dev));
+  struct copy_job jobs[16];
+  pthread_t tid[16];
+  size_t slice = ((bytes / (size_t)nthreads) + 4095) & ~(size_t)4095;
+  int n = 0;
+  for (size_t off = 0; off < bytes && n < nthreads; off += slice, ++n) {
+    jobs[n].dst = (char *)dst + off;
+    jobs[n].src = (const char *)src + off;
+    jobs[n].bytes = bytes - off < slice ? bytes - off : slice;
+    jobs[n].device = dev;
+    jobs[n].err = hipSuccess;
+  }
+  int started = 0;
+  for (int i = 1; i < n; ++i, ++started)
+    if (pthread_create(&tid[i], NULL, copy_thread, &jobs[i])) break;
+  copy_thread(&jobs[0]);
+  for (int i = 1; i <= started; ++i) pthread_join(tid[i], NULL);
+  for (int i = started + 1; i < n; ++i) copy_thread(&jobs[i]);   /* threads that failed to start */
+  for (int i = 0; i < n; ++i)
+    if (jobs[i].err != hipSuccess) { pg_set_error("copy: %s", hipGetErrorString(jobs[i].err)); return -1; }
+  return 0;
+}
+
 static int copy_any(void *dst, const void *src, size_t bytes) {
   if (!bytes || dst == src) return 0;
-  if (!is_device_ptr(dst) && !is_device_ptr(src)) { memmove(dst, src, bytes); return 0; }
+  int dd = is_device_ptr(dst), sd = is_device_ptr(src);
+  if (!dd && !sd) { memmove(dst, src, bytes); return 0; }
+  if (dd != sd) return pg_copy_parallel(dst, src, bytes);      /* crosses PCIe */
   PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
   return 0;
 }
@@ -540,48 +599,39 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
 
 /* ---- host-memory reduce (the arriving-chunk step with host buffers) ------------ */
 
-/* dst[i] = dst[i] op src[i] with dst/src in host memory: chunked through HBM on
- * two streams, so chunk k's copies overlap chunk k-1's reduce and write-back.
- * Measures the PCIe-inclusive rate of the hot path (DESIGN.md §Host path). */
+/* dst[i] = dst[i] op src[i] with dst/src in host memory, staged through HBM
+ * in pieces of chunk_bytes (default 256 MiB): threaded H2D of both operands
+ * (pg_copy_parallel), the reduce, threaded D2H.  Measures the PCIe-inclusive
+ * rate of the hot path. */
 int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes) {
   size_t es = pg_elem_size(datatype);
   if (!es || (op != PGK_OP_SUM && op != PGK_OP_PROD)) { pg_set_error("pgx_reduce_host: bad datatype/op"); return -1; }
   if (!n) return 0;
   if (!dst || !src) { pg_set_error("pgx_reduce_host: NULL buffer"); return -1; }
-  if (chunk_bytes < (1u << 20)) chunk_bytes = 64u << 20;
+  if (chunk_bytes < (1u << 20)) chunk_bytes = 256u << 20;
   size_t ce = chunk_bytes / es;
-  hipStream_t st[2] = {NULL, NULL};
-  void *dd[2] = {NULL, NULL}, *ds[2] = {NULL, NULL};
+  if (ce > n) ce = n;
+  hipStream_t st = NULL;
+  void *dd = NULL, *ds = NULL;
   int rc = -1;
-  for (int i = 0; i < 2; ++i) {
-    if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&dd[i], ce * es) != hipSuccess || hipMalloc(&ds[i], ce * es) != hipSuccess) {
-      pg_set_error("pgx_reduce_host: HIP allocation failed");
-      goto out;
-    }
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipMalloc(&dd, ce * es) != hipSuccess ||
+      hipMalloc(&ds, ce * es) != hipSuccess) {
+    pg_set_error("pgx_reduce_host: HIP allocation failed");
+    goto out;
   }
-  for (size_t off = 0, k = 0; off < n; off += ce, ++k) {
+  for (size_t off = 0; off < n; off += ce) {
     size_t m = n - off < ce ? n - off : ce;
-    int s = (int)(k & 1);
     char *hd = (char *)dst + off * es;
     const char *hs = (const char *)src + off * es;
-    if (hipMemcpyAsync(dd[s], hd, m * es, hipMemcpyHostToDevice, st[s]) != hipSuccess ||
-        hipMemcpyAsync(ds[s], hs, m * es, hipMemcpyHostToDevice, st[s]) != hipSuccess) {
-      pg_set_error("pgx_reduce_host: H2D failed");
-      goto out;
-    }
-    if (pgk_reduce(dd[s], ds[s], m, datatype, op, (void *)st[s])) { pg_set_error("%s", pgk_last_error()); goto out; }
-    if (hipMemcpyAsync(hd, dd[s], m * es, hipMemcpyDeviceToHost, st[s]) != hipSuccess) {
-      pg_set_error("pgx_reduce_host: D2H failed");
-      goto out;
-    }
+    if (pg_copy_parallel(dd, hd, m * es) || pg_copy_parallel(ds, hs, m * es)) goto out;
+    if (pgk_reduce(dd, ds, m, datatype, op, (void *)st)) { pg_set_error("%s", pgk_last_error()); goto out; }
+    if (pg_stream_wait(st)) goto out;
+    if (pg_copy_parallel(hd, dd, m * es)) goto out;
   }
   rc = 0;
 out:
-  for (int i = 0; i < 2; ++i) {
-    if (st[i]) { hipStreamSynchronize(st[i]); hipStreamDestroy(st[i]); }
-    if (dd[i]) hipFree(dd[i]);
-    if (ds[i]) hipFree(ds[i]);
-  }
+  if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+  if (dd) hipFree(dd);
+  if (ds) hipFree(ds);
   return rc;
 }

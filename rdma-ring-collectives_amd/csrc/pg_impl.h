@@ -74,6 +74,7 @@ struct pg_impl {
 void pg_set_error(const char *fmt, ...);
 int pg_ensure(void **buf, size_t *cap, size_t bytes);   /* hipMalloc-grow */
 int pg_stream_wait(hipStream_t s);                        /* bounded spin, then block */
+int pg_copy_parallel(void *dst, const void *src, size_t bytes);  /* host<->device, threaded */
 int pg_impl_create(struct pg *pg);                        /* streams/events */
 void pg_impl_destroy(struct pg *pg);
 size_t pg_elem_size(int dt);

@@ -178,9 +178,10 @@ static int publish(struct pg *pg, const void *src, size_t bytes, int src_dev, ch
       const void *sv[1] = {src};
       size_t nb[1] = {bytes};
       if (pgk_gather(d, sv, nb, 1, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
+    } else if (!src_dev) {
+      if (pg_copy_parallel(*xslot, src, bytes)) return -1;
     } else {
-      PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                  im->red));
+      PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, hipMemcpyDeviceToDevice, im->red));
     }
     if (pg_stream_wait(im->red)) return -1;
   }
@@ -229,7 +230,7 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   if (fold_block(pg, out, (int)(x->gen & 1), off, len, dt, op)) return -1;
   if (pg_stream_wait(im->red)) return -1;
   im->stats.kernel_us += us_now() - tk;
-  if (!rd && len) PG_CHECK_HIP(hipMemcpy(recvbuf, out, len * es, hipMemcpyDeviceToHost));
+  if (!rd && len && pg_copy_parallel(recvbuf, out, len * es)) return -1;
   x->gen++;
   return 0;
 }
@@ -274,7 +275,7 @@ int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     full = (char *)im->dout;
   }
   if (gather(pg, full, (int)(x->gen & 1), count, 1, dt)) return -1;
-  if (!rd && total) PG_CHECK_HIP(hipMemcpy(recvbuf, full, total, hipMemcpyDeviceToHost));
+  if (!rd && total && pg_copy_parallel(recvbuf, full, total)) return -1;
   im->stats.bytes_recv += (int64_t)(total - slot_bytes);
   x->gen++;
   return 0;
@@ -307,7 +308,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     }
     if (pg_stream_wait(im->red)) return -1;
     im->stats.kernel_us += us_now() - tk;
-    if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
+    if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
     x->gen++;
     return 0;
   }
@@ -327,7 +328,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   double tg = us_now();
   if (gather(pg, full, 2 + which, count, 0, dt)) return -1;
   im->stats.kernel_us += us_now() - tg;
-  if (!rd && bytes) PG_CHECK_HIP(hipMemcpy(recvbuf, full, bytes, hipMemcpyDeviceToHost));
+  if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
   x->gen++;
   return 0;
 }
