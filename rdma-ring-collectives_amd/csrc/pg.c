@@ -202,6 +202,8 @@ void pg_impl_destroy(struct pg *pg) {
   im->boot_fds = NULL;
   for (int i = 0; i < im->n_red_ev; ++i) hipEventDestroy(im->red_ev[i]);
   free(im->red_ev);
+  for (int i = 0; i < im->n_round_ev; ++i) hipEventDestroy(im->round_ev[i]);
+  free(im->round_ev);
   for (int i = 0; i < PG_RECV_EVENTS; ++i) if (im->recv_ev[i]) hipEventDestroy(im->recv_ev[i]);
   if (im->join_ev) hipEventDestroy(im->join_ev);
   if (im->t0) hipEventDestroy(im->t0);
@@ -328,6 +330,61 @@ static int ensure_stage(struct pg_impl *im, int count, int dt) {
   return pg_ensure(&im->stage[1], &cap1, bytes);
 }
 
+/* ---- host-staging pipeline ----------------------------------------------------
+ * Host buffers are moved block by block between the ring rounds instead of
+ * whole up front: before round k the host uploads the source blocks that
+ * round first reads (round 0 sends block r-1 and every round k reduces into
+ * block r-2-k), while the GPU is still moving round k-1; an all-gather's
+ * arrived block is downloaded while the next round is on the wire.  Plain
+ * (pageable) hipMemcpy is synchronous for the host thread but runs beside the
+ * non-blocking comm/reduce streams. */
+struct stage_ctx {
+  const char *host_src;   /* upload source (host), NULL: nothing to upload      */
+  char *dev_src;          /* device image of the source                        */
+  char *host_dst;         /* download target (host), NULL: nothing to download */
+  char *dev_dst;          /* device image of the result                        */
+  int count, dt, uniform; /* block geometry (uniform: AG blocks of `count`)     */
+  unsigned char *up;      /* uploaded flags per block                          */
+  double *h2d_us, *d2h_us;
+};
+
+static void stage_block(const struct stage_ctx *c, int world, int b, size_t *off, size_t *len) {
+  if (c->uniform) { *off = (size_t)b * (size_t)c->count; *len = (size_t)c->count; }
+  else pg_block_range(c->count, world, b, off, len);
+}
+
+static int upload_block(struct pg *pg, struct stage_ctx *c, int b) {
+  b = ((b % pg->world_size) + pg->world_size) % pg->world_size;
+  if (!c->host_src || c->up[b]) return 0;
+  size_t es = pg_elem_size(c->dt), off, len;
+  stage_block(c, pg->world_size, b, &off, &len);
+  c->up[b] = 1;
+  return len ? timed_copy(c->dev_src + off * es, c->host_src + off * es, len * es, c->h2d_us) : 0;
+}
+
+/* reduce-scatter rounds: round k reads source blocks r-1 (k = 0, sent) and r-2-k */
+static int rs_upload_hook(struct pg_impl *im, void *ctx, int k) {
+  struct pg *pg = im->pg;
+  struct stage_ctx *c = (struct stage_ctx *)ctx;
+  if (k >= pg->world_size - 1) return 0;
+  if (k == 0 && upload_block(pg, c, pg->rank - 1)) return -1;
+  if (upload_block(pg, c, pg->rank - 2 - k)) return -1;
+  if (k == 0 && upload_block(pg, c, pg->rank - 3)) return -1;   /* one block of lead */
+  return 0;
+}
+
+/* all-gather rounds: round k receives block r-k-1; download it once round k is done */
+static int ag_download_hook(struct pg_impl *im, void *ctx, int k) {
+  struct pg *pg = im->pg;
+  struct stage_ctx *c = (struct stage_ctx *)ctx;
+  if (!c->host_dst || k == 0) return 0;
+  PG_CHECK_HIP(hipEventSynchronize(im->round_ev[k - 1]));
+  int b = ((pg->rank - k) % pg->world_size + pg->world_size) % pg->world_size;   /* block of round k-1 */
+  size_t es = pg_elem_size(c->dt), off, len;
+  stage_block(c, pg->world_size, b, &off, &len);
+  return len ? timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us) : 0;
+}
+
 /* ---- reduce-scatter ---------------------------------------------------------- */
 
 static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
@@ -338,10 +395,25 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
   if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());   /* caller's producers */
 
   void *src = sendbuf;
+  unsigned char up[64];
+  struct stage_ctx sc;
+  memset(&sc, 0, sizeof(sc));
+  int lazy = !sd && pg->world_size <= 64;
   if (!sd) {
     if (pg_ensure(&im->dsrc, &im->dsrc_cap, (size_t)count * es)) return -1;
-    if (timed_copy(im->dsrc, sendbuf, (size_t)count * es, &im->stats.h2d_us)) return -1;
     src = im->dsrc;
+    if (lazy) {                   /* blocks go up between rounds (rs_upload_hook) */
+      memset(up, 0, sizeof(up));
+      sc.host_src = (const char *)sendbuf;
+      sc.dev_src = (char *)src;
+      sc.count = count;
+      sc.dt = dt;
+      sc.up = up;
+      sc.h2d_us = &im->stats.h2d_us;
+      sc.d2h_us = &im->stats.d2h_us;
+    } else if (timed_copy(im->dsrc, sendbuf, (size_t)count * es, &im->stats.h2d_us)) {
+      return -1;
+    }
   }
   void *out = recvbuf;
   int post_copy = 0;
@@ -355,7 +427,7 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
   if (n < 0) return -1;
   void *bufs[5] = {NULL, src, out, im->stage[0], im->stage[1]};
   PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
-  if (pg_exec_plan(im, im->steps, n, bufs, dt, op)) return -1;
+  if (pg_exec_plan(im, im->steps, n, bufs, dt, op, lazy ? rs_upload_hook : NULL, &sc)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
   if (sync_ring(im, 1)) return -1;
   if (post_copy && timed_copy(recvbuf, out, blen * es, &im->stats.d2h_us)) return -1;
@@ -470,11 +542,21 @@ static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   int n = plan_into(im, 0, count, dt, 0, 1);
   if (n < 0) return -1;
   void *bufs[5] = {NULL, NULL, full, NULL, NULL};
+  struct stage_ctx sc;
+  memset(&sc, 0, sizeof(sc));
+  sc.host_dst = rd ? NULL : (char *)recvbuf;
+  sc.dev_dst = full;
+  sc.count = count;
+  sc.dt = dt;
+  sc.uniform = 1;
+  sc.d2h_us = &im->stats.d2h_us;
   PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
-  if (pg_exec_plan(im, im->steps, n, bufs, dt, PGK_OP_SUM)) return -1;
+  if (pg_exec_plan(im, im->steps, n, bufs, dt, PGK_OP_SUM, rd ? NULL : ag_download_hook, &sc)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
   if (sync_ring(im, 1)) return -1;
-  if (!rd && timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
+  /* the hook downloaded every received block as its round completed; this
+   * rank's own block is still only on the device */
+  if (!rd && timed_copy((char *)recvbuf + (size_t)pg->rank * slot, own, slot, &im->stats.d2h_us)) return -1;
   return 0;
 }
 
@@ -545,24 +627,50 @@ static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int coun
     if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
     work = (char *)im->dout;
   }
+  /* the input reaches `work` either by a device copy, or -- from host memory
+   * -- block by block between the reduce-scatter rounds */
+  const void *host_in = NULL;
   if (sendbuf != recvbuf) {
-    if (timed_copy(work, sendbuf, bytes, sd ? &im->stats.ring_us : &im->stats.h2d_us)) return -1;
+    if (sd) { if (timed_copy(work, sendbuf, bytes, &im->stats.ring_us)) return -1; }
+    else host_in = sendbuf;
   } else if (!rd) {
-    if (timed_copy(work, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+    host_in = recvbuf;
+  }
+  if (host_in && pg->world_size > 64) {
+    if (timed_copy(work, host_in, bytes, &im->stats.h2d_us)) return -1;
+    host_in = NULL;
   }
   if (ensure_stage(im, count, dt)) return -1;
+  unsigned char up[64];
+  memset(up, 0, sizeof(up));
+  struct stage_ctx sc;
+  memset(&sc, 0, sizeof(sc));
+  sc.host_src = (const char *)host_in;
+  sc.dev_src = work;
+  sc.host_dst = rd ? NULL : (char *)recvbuf;
+  sc.dev_dst = work;
+  sc.count = count;
+  sc.dt = dt;
+  sc.up = up;
+  sc.h2d_us = &im->stats.h2d_us;
+  sc.d2h_us = &im->stats.d2h_us;
   PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
   int n = plan_into(im, 1, count, dt, 1, 0);
   if (n < 0) return -1;
   void *rs_bufs[5] = {NULL, work, work + boff * es, im->stage[0], im->stage[1]};
-  if (pg_exec_plan(im, im->steps, n, rs_bufs, dt, op)) return -1;
+  if (pg_exec_plan(im, im->steps, n, rs_bufs, dt, op, host_in ? rs_upload_hook : NULL, &sc)) return -1;
+  /* the in-place fold of the last round reads block `rank` itself */
+  if (host_in && upload_block(pg, &sc, pg->rank)) return -1;
   n = plan_into(im, 0, count, dt, 0, 0);
   if (n < 0) return -1;
   void *ag_bufs[5] = {NULL, NULL, work, NULL, NULL};
-  if (pg_exec_plan(im, im->steps, n, ag_bufs, dt, op)) return -1;
+  if (pg_exec_plan(im, im->steps, n, ag_bufs, dt, op, rd ? NULL : ag_download_hook, &sc)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
   if (sync_ring(im, 1)) return -1;
-  if (!rd && timed_copy(recvbuf, work, bytes, &im->stats.d2h_us)) return -1;
+  /* received blocks were downloaded round by round; this rank's own block
+   * (reduced here) is still only on the device */
+  if (!rd && blen && timed_copy((char *)recvbuf + boff * es, work + boff * es, blen * es, &im->stats.d2h_us))
+    return -1;
   return 0;
 }
 

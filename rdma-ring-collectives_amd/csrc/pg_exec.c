@@ -46,9 +46,26 @@ static inline char *at(void *const bufs[5], int which, int64_t off) {
   return (char *)bufs[which] + off;
 }
 
+static int ensure_round_events(struct pg_impl *im, int need) {
+  if (need <= im->n_round_ev) return 0;
+  hipEvent_t *ev = (hipEvent_t *)realloc(im->round_ev, sizeof(hipEvent_t) * (size_t)need);
+  if (!ev) { pg_set_error("pg_exec: out of host memory"); return -1; }
+  im->round_ev = ev;
+  for (int i = im->n_round_ev; i < need; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&im->round_ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      im->n_round_ev = i;
+      pg_set_error("pg_exec: hipEventCreate: %s", hipGetErrorString(e));
+      return -1;
+    }
+  }
+  im->n_round_ev = need;
+  return 0;
+}
+
 int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
-                 void *const bufs[5], int dt, int op) {
-  if (n <= 0) return 0;
+                 void *const bufs[5], int dt, int op, pg_round_hook hook, void *hook_ctx) {
+  if (n <= 0) return hook ? hook(im, hook_ctx, 0) : 0;
   const struct pg *pg = im->pg;
   const int right = (pg->rank + 1) % pg->world_size;
   const int left = (pg->rank - 1 + pg->world_size) % pg->world_size;
@@ -57,10 +74,17 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
   for (int i = 0; i < n; ++i) if (st[i].seg > max_seg) max_seg = st[i].seg;
   if (ensure_red_events(im, max_seg + 1)) return -1;
 
-  int i = 0, nb = 0;
+  int rounds = st[n - 1].round + 1;
+  if (hook && ensure_round_events(im, rounds)) return -1;
+  int i = 0, nb = 0, cur_round = -1;
   while (i < n) {
     int b = st[i].batch, j = i;
     while (j < n && st[j].batch == b) ++j;          /* steps [i, j) = one batch */
+    if (hook && st[i].round != cur_round) {
+      if (cur_round >= 0) PG_CHECK_HIP(hipEventRecord(im->round_ev[cur_round], im->comm));
+      cur_round = st[i].round;
+      if (hook(im, hook_ctx, cur_round)) return -1;
+    }
 
     /* forwarded partials must be reduced before they go on the wire */
     for (int s = i; s < j; ++s)
@@ -118,6 +142,10 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
     }
     ++nb;
     i = j;
+  }
+  if (hook) {
+    PG_CHECK_HIP(hipEventRecord(im->round_ev[cur_round], im->comm));
+    if (hook(im, hook_ctx, cur_round + 1)) return -1;
   }
   /* join: the comm stream observes the last reduce */
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));

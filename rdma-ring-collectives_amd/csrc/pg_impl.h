@@ -59,6 +59,8 @@ struct pg_impl {
   int n_red_ev;
   hipEvent_t recv_ev[PG_RECV_EVENTS]; /* per batch: its receives landed       */
   hipEvent_t join_ev, t0, t1;
+  hipEvent_t *round_ev;       /* per ring round: its transfers are enqueued-done */
+  int n_round_ev;
 
   /* HBM working memory, grown on demand and kept (288 GB per GPU). */
   void *stage[2];  size_t stage_cap;
@@ -79,9 +81,14 @@ int pg_impl_create(struct pg *pg);                        /* streams/events */
 void pg_impl_destroy(struct pg *pg);
 size_t pg_elem_size(int dt);
 
-/* pg_exec.c: run `n` steps; bufs[] indexed by PG_BUF_*. */
+/* pg_exec.c: run `n` steps; bufs[] indexed by PG_BUF_*.  If `hook` is set it
+ * is called on the host before the first batch of each round k (and once with
+ * k = rounds after the last), after round_ev[k-1] -- recorded on the comm
+ * stream behind round k-1's transfers -- exists: the host-staging pipeline
+ * uploads/downloads blocks there while the GPU runs the ring. */
+typedef int (*pg_round_hook)(struct pg_impl *im, void *ctx, int round);
 int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
-                 void *const bufs[5], int dt, int op);
+                 void *const bufs[5], int dt, int op, pg_round_hook hook, void *hook_ctx);
 
 /* pg_xport_rccl.c */
 int pg_xport_rccl_init(struct pg *pg);
