@@ -345,6 +345,7 @@ struct stage_ctx {
   char *dev_dst;          /* device image of the result                        */
   int count, dt, uniform; /* block geometry (uniform: AG blocks of `count`)     */
   unsigned char *up;      /* uploaded flags per block                          */
+  int next_dl;            /* first all-gather round whose block is not downloaded */
   double *h2d_us, *d2h_us;
 };
 
@@ -373,16 +374,25 @@ static int rs_upload_hook(struct pg_impl *im, void *ctx, int k) {
   return 0;
 }
 
-/* all-gather rounds: round k receives block r-k-1; download it once round k is done */
+/* all-gather rounds: round j receives block r-j-1.  Before round k starts,
+ * every round < k has been enqueued; wait for the last recorded one (stream
+ * order covers the earlier ones) and download the blocks of rounds
+ * next_dl .. k-1.  Called with k = world-1 after the last round.  Rounds that
+ * had no steps (empty blocks) have nothing to download. */
 static int ag_download_hook(struct pg_impl *im, void *ctx, int k) {
   struct pg *pg = im->pg;
   struct stage_ctx *c = (struct stage_ctx *)ctx;
-  if (!c->host_dst || k == 0) return 0;
-  PG_CHECK_HIP(hipEventSynchronize(im->round_ev[k - 1]));
-  int b = ((pg->rank - k) % pg->world_size + pg->world_size) % pg->world_size;   /* block of round k-1 */
-  size_t es = pg_elem_size(c->dt), off, len;
-  stage_block(c, pg->world_size, b, &off, &len);
-  return len ? timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us) : 0;
+  if (!c->host_dst || c->next_dl >= k) return 0;
+  if (im->last_round_rec >= 0) PG_CHECK_HIP(hipEventSynchronize(im->round_ev[im->last_round_rec]));
+  size_t es = pg_elem_size(c->dt);
+  for (int j = c->next_dl; j < k; ++j) {
+    int b = ((pg->rank - j - 1) % pg->world_size + pg->world_size) % pg->world_size;
+    size_t off, len;
+    stage_block(c, pg->world_size, b, &off, &len);
+    if (len && timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us)) return -1;
+  }
+  c->next_dl = k;
+  return 0;
 }
 
 /* ---- reduce-scatter ---------------------------------------------------------- */

@@ -42,6 +42,8 @@ static int ensure_red_events(struct pg_impl *im, int need) {
   return 0;
 }
 
+static int pg_world_of(const struct pg_impl *im) { return im->pg->world_size; }
+
 static inline char *at(void *const bufs[5], int which, int64_t off) {
   return (char *)bufs[which] + off;
 }
@@ -65,7 +67,10 @@ static int ensure_round_events(struct pg_impl *im, int need) {
 
 int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
                  void *const bufs[5], int dt, int op, pg_round_hook hook, void *hook_ctx) {
-  if (n <= 0) return hook ? hook(im, hook_ctx, 0) : 0;
+  if (n <= 0) {
+    im->last_round_rec = -1;
+    return hook ? hook(im, hook_ctx, pg_world_of(im) - 1) : 0;
+  }
   const struct pg *pg = im->pg;
   const int right = (pg->rank + 1) % pg->world_size;
   const int left = (pg->rank - 1 + pg->world_size) % pg->world_size;
@@ -76,12 +81,16 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
 
   int rounds = st[n - 1].round + 1;
   if (hook && ensure_round_events(im, rounds)) return -1;
+  im->last_round_rec = -1;
   int i = 0, nb = 0, cur_round = -1;
   while (i < n) {
     int b = st[i].batch, j = i;
     while (j < n && st[j].batch == b) ++j;          /* steps [i, j) = one batch */
     if (hook && st[i].round != cur_round) {
-      if (cur_round >= 0) PG_CHECK_HIP(hipEventRecord(im->round_ev[cur_round], im->comm));
+      if (cur_round >= 0) {
+        PG_CHECK_HIP(hipEventRecord(im->round_ev[cur_round], im->comm));
+        im->last_round_rec = cur_round;
+      }
       cur_round = st[i].round;
       if (hook(im, hook_ctx, cur_round)) return -1;
     }
@@ -145,7 +154,8 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
   }
   if (hook) {
     PG_CHECK_HIP(hipEventRecord(im->round_ev[cur_round], im->comm));
-    if (hook(im, hook_ctx, cur_round + 1)) return -1;
+    im->last_round_rec = cur_round;
+    if (hook(im, hook_ctx, pg->world_size - 1)) return -1;   /* after the last round */
   }
   /* join: the comm stream observes the last reduce */
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));

@@ -59,8 +59,9 @@ struct pg_impl {
   int n_red_ev;
   hipEvent_t recv_ev[PG_RECV_EVENTS]; /* per batch: its receives landed       */
   hipEvent_t join_ev, t0, t1;
-  hipEvent_t *round_ev;       /* per ring round: its transfers are enqueued-done */
+  hipEvent_t *round_ev;       /* per ring round: recorded behind its transfers */
   int n_round_ev;
+  int last_round_rec;         /* round whose round_ev was recorded last, -1: none */
 
   /* HBM working memory, grown on demand and kept (288 GB per GPU). */
   void *stage[2];  size_t stage_cap;

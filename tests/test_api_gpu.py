@@ -200,6 +200,7 @@ CASES = [  # world, dt, op, count, chunk_bytes, eager_max, inflight
     (4, 1, 0, 100003, 1 << 16, 4096, 4), (4, 0, 1, 4096, 4096, 4096, 1), (4, 1, 1, 5, 8, 0, 2),
     (8, 1, 0, 65536 + 3, 1 << 14, 0, 4), (8, 0, 0, 8, 4, 0, 1), (8, 1, 1, 1001, 128, 0, 8),
     (5, 1, 0, 12345, 2048, 4096, 2),
+    (8, 1, 0, 3, 64, 0, 1), (6, 0, 1, 2, 8, 0, 2),     # count < W: several empty blocks, skipped rounds
 ]
 
 
