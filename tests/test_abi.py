@@ -75,3 +75,18 @@ def test_connect_without_gpu_fails_cleanly(lib):
         return  # a GPU machine: covered by the gpu tests
     h = ctypes.c_void_p()
     assert lib.connect_process_group(b"nosuchhost-xyz", ctypes.byref(h)) == -1
+
+
+def test_headers_compile_as_c_and_cpp(tmp_path):
+    """The three public headers are self-contained C and usable from C++
+    (extern "C" guards), and `make install` lays out a drop-in prefix."""
+    src = tmp_path / "h.c"
+    src.write_text('#include "pg.h"\n#include "pg_ext.h"\n#include "pgk.h"\nint main(void){return 0;}\n')
+    inc = str(pgamd.REPO_ROOT / "include")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", inc, str(src), "-o", str(tmp_path / "hc")], check=True)
+    cpp = tmp_path / "h.cpp"
+    cpp.write_text(src.read_text())
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, str(cpp), "-o", str(tmp_path / "hcpp")], check=True)
+    subprocess.run(["make", "-s", "-C", str(pgamd.PKG_DIR), "install", f"DESTDIR={tmp_path}", "PREFIX=/opt/pg"],
+                   check=True)
+    assert (tmp_path / "opt/pg/lib/libpg_amd.so").exists() and (tmp_path / "opt/pg/include/pg.h").exists()
