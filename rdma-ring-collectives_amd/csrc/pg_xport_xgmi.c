@@ -28,6 +28,13 @@
 #include "pg_impl.h"
 
 #define XG_SLOTS 4              /* X0, X1, R0, R1 */
+#define XG_IMPORTS 2            /* mapped input allocations cached per peer */
+
+struct xg_import {
+  unsigned long long bid;
+  void *base;
+  unsigned long stamp;
+};
 #define XG_GRANULE (64ull << 20)
 
 struct xgmi_ctx {
@@ -36,8 +43,17 @@ struct xgmi_ctx {
   void **peer;                  /* peer[q] = rank q's allocation, mapped    */
   size_t oneshot_max;           /* all-reduce at most this many bytes: one-shot */
   void *bar;                    /* node-local shm barrier (pg_boot.c), or NULL */
+  int zc;                       /* zero-copy inputs allowed (PG_XGMI_ZERO_COPY) */
+  hipIpcMemHandle_t exp_h;      /* last export of a caller allocation       */
+  unsigned long long exp_bid;
+  void *exp_base;
+  int exp_valid;
+  struct xg_import *imp;        /* world * XG_IMPORTS mapped peer inputs     */
+  unsigned long clock;
   unsigned long gen;            /* collective calls so far (slot parity)    */
 };
+
+static void drop_imports(struct pg *pg, struct xgmi_ctx *x);
 
 static struct xgmi_ctx *ctx_of(struct pg *pg) {
   return (struct xgmi_ctx *)((struct pg_impl *)pg->impl)->xctx;
@@ -134,6 +150,10 @@ int pg_xport_xgmi_init(struct pg *pg) {
   x->oneshot_max = 1u << 20;
   const char *e = getenv("PG_ONESHOT_MAX");
   if (e && *e) x->oneshot_max = (size_t)strtoull(e, NULL, 0);
+  e = getenv("PG_XGMI_ZERO_COPY");
+  x->zc = !(e && *e == '0');
+  x->imp = (struct xg_import *)calloc((size_t)pg->world_size * XG_IMPORTS, sizeof(struct xg_import));
+  if (!x->imp) { pg_set_error("xgmi: out of host memory"); return -1; }
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
   const char *nb = getenv("PG_NO_SHM_BARRIER");
   if (!(nb && *nb == '1') && pg_shm_open(pg, im->boot_fds, &x->bar)) return -1;
@@ -146,6 +166,8 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   if (!x) return;
   /* peers may still be reading my last contribution: meet them first */
   if (x->mem && im->boot_fds) barrier(pg);
+  drop_imports(pg, x);
+  free(x->imp);
   unmap(pg, x);
   pg_shm_close(x->bar);
   free(x->peer);
@@ -161,89 +183,214 @@ static int is_dev(const void *p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
 }
 
-/* Copy this rank's contribution into X[parity] and meet the other ranks. */
-static int publish(struct pg *pg, const void *src, size_t bytes, int src_dev, char **xslot) {
+/* ---- sharing the inputs -------------------------------------------------------
+ * Every rank must be able to read every other rank's input.  Two ways:
+ *  - zero-copy: the caller's own device allocation is exported through HIP
+ *    IPC (cached by HIP buffer id on both sides), with descriptors in the
+ *    node-local shm page; used when every rank's input is device memory that
+ *    exports and the output does not overlap the input.  A closing barrier
+ *    keeps inputs untouched until every peer has finished reading them.
+ *  - slot copy: the input is copied into this rank's X[parity] slot.
+ * The choice is collective: each rank flags whether its export worked, and
+ * after the first barrier every rank sees the same flags. */
+#define XG_DESC_OFF 256          /* descriptor table offset in the shm page */
+
+struct xg_desc {
+  hipIpcMemHandle_t h;
+  uint64_t bid;                  /* HIP buffer id of the exported allocation */
+  uint64_t off;                  /* input offset inside it                    */
+  int32_t ok;
+  int32_t pad;
+};
+
+static struct xg_desc *descs(struct xgmi_ctx *x) {
+  return (struct xg_desc *)((char *)x->bar + XG_DESC_OFF);
+}
+
+static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
+  memset(d, 0, sizeof(*d));
+  void *base = NULL;
+  size_t size = 0;
+  unsigned long long bid = 0;
+  if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &size, (hipDeviceptr_t)in) != hipSuccess ||
+      hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)in) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (!x->exp_valid || x->exp_bid != bid || x->exp_base != base) {
+    x->exp_valid = 0;
+    if (hipIpcGetMemHandle(&x->exp_h, base) != hipSuccess) { (void)hipGetLastError(); return 0; }
+    x->exp_bid = bid;
+    x->exp_base = base;
+    x->exp_valid = 1;
+  }
+  d->h = x->exp_h;
+  d->bid = bid;
+  d->off = (uint64_t)((const char *)in - (const char *)base);
+  d->ok = 1;
+  return 1;
+}
+
+/* Peer q's input, mapped (LRU cache of XG_IMPORTS allocations per peer). */
+static const char *import_input(struct xgmi_ctx *x, int q, const struct xg_desc *d) {
+  struct xg_import *e = &x->imp[q * XG_IMPORTS];
+  int lru = 0;
+  ++x->clock;
+  for (int i = 0; i < XG_IMPORTS; ++i) {
+    if (e[i].base && e[i].bid == d->bid) { e[i].stamp = x->clock; return (const char *)e[i].base + d->off; }
+    if (e[i].stamp < e[lru].stamp) lru = i;
+  }
+  if (e[lru].base) { hipIpcCloseMemHandle(e[lru].base); e[lru].base = NULL; }
+  void *p = NULL;
+  if (hipIpcOpenMemHandle(&p, d->h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    (void)hipGetLastError();
+    return NULL;
+  }
+  e[lru].base = p;
+  e[lru].bid = d->bid;
+  e[lru].stamp = x->clock;
+  return (const char *)p + d->off;
+}
+
+static void drop_imports(struct pg *pg, struct xgmi_ctx *x) {
+  if (!x->imp) return;
+  for (int i = 0; i < pg->world_size * XG_IMPORTS; ++i)
+    if (x->imp[i].base) { hipIpcCloseMemHandle(x->imp[i].base); x->imp[i].base = NULL; }
+}
+
+/* Make every rank's input readable; by_rank[q] = where rank q's input starts.
+ * *zero_copy tells the caller to close with barrier(); *fail = this rank could
+ * not map a peer (it must still join that barrier, then report -1). */
+static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev, int may_alias_out,
+                        const char **by_rank, int *zero_copy, int *fail) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
-  int which = (int)(x->gen & 1);
-  *xslot = slot(x, pg->rank, which);
+  const int W = pg->world_size, r = pg->rank, which = (int)(x->gen & 1);
+  *zero_copy = 0;
+  *fail = 0;
   double t0 = us_now();
-  if (src_dev) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  if (in_dev) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
   double t1 = us_now();
+  im->stats.sync_us += t1 - t0;
+  if (x->zc && x->bar && bytes) {
+    struct xg_desc mine;
+    if (!in_dev || may_alias_out || !export_input(x, in, &mine)) memset(&mine, 0, sizeof(mine));
+    descs(x)[r] = mine;
+    if (barrier(pg)) return -1;
+    struct xg_desc all[16];
+    memcpy(all, descs(x), sizeof(struct xg_desc) * (size_t)W);
+    int all_ok = 1;
+    for (int q = 0; q < W; ++q) all_ok &= all[q].ok;
+    im->stats.barrier_us += us_now() - t1;
+    if (all_ok) {
+      for (int q = 0; q < W; ++q) {
+        by_rank[q] = q == r ? (const char *)in : import_input(x, q, &all[q]);
+        if (!by_rank[q]) {
+          pg_set_error("xgmi: could not map rank %d's input", q);
+          *fail = 1;
+        }
+      }
+      *zero_copy = 1;
+      return 0;
+    }
+    /* somebody's input cannot be shared in place: everybody copies */
+  }
+  char *xs = slot(x, r, which);
+  double t2 = us_now();
   if (bytes) {
-    if (src_dev && ((uintptr_t)src & 3) == 0 && (bytes & 3) == 0) {
+    if (in_dev && ((uintptr_t)in & 3) == 0 && (bytes & 3) == 0) {
       /* device input: a copy kernel (the DMA engine path costs ~50 us to
        * start for a small copy) */
-      void *d[1] = {*xslot};
-      const void *sv[1] = {src};
+      void *d[1] = {xs};
+      const void *sv[1] = {in};
       size_t nb[1] = {bytes};
       if (pgk_gather(d, sv, nb, 1, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
-    } else if (!src_dev) {
-      if (pg_copy_parallel(*xslot, src, bytes)) return -1;
+    } else if (!in_dev) {
+      if (pg_copy_parallel(xs, in, bytes)) return -1;
     } else {
-      PG_CHECK_HIP(hipMemcpyAsync(*xslot, src, bytes, hipMemcpyDeviceToDevice, im->red));
+      PG_CHECK_HIP(hipMemcpyAsync(xs, in, bytes, hipMemcpyDeviceToDevice, im->red));
     }
     if (pg_stream_wait(im->red)) return -1;
   }
-  double t2 = us_now();
+  double t3 = us_now();
   int rc = barrier(pg);
-  im->stats.sync_us += t1 - t0;
-  im->stats.copy_us += t2 - t1;
-  im->stats.barrier_us += us_now() - t2;
+  im->stats.copy_us += t3 - t2;
+  im->stats.barrier_us += us_now() - t3;
+  for (int q = 0; q < W; ++q) by_rank[q] = slot(x, q, which);
   return rc;
 }
 
-/* out = fold over ranks, in ring order, of block `b` of slot `which`. */
-static int fold_block(struct pg *pg, void *out, int which, size_t off_elems, size_t len, int dt, int op) {
-  struct pg_impl *im = (struct pg_impl *)pg->impl;
+/* End of a call: zero-copy inputs stay untouched until every peer is done. */
+static int finish(struct pg *pg, int zero_copy, int fail) {
   struct xgmi_ctx *x = ctx_of(pg);
+  int rc = 0;
+  if (zero_copy) {
+    struct pg_impl *im = (struct pg_impl *)pg->impl;
+    double t = us_now();
+    rc = barrier(pg);
+    im->stats.barrier_us += us_now() - t;
+  }
+  x->gen++;
+  return (rc || fail) ? -1 : 0;
+}
+
+/* out = fold over ranks, in ring order, of the block at off_elems. */
+static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size_t off_elems, size_t len, int dt,
+                      int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
   if (!len) return 0;
   int W = pg->world_size, r = pg->rank;
   size_t es = pg_elem_size(dt);
   const void *srcs[16];
-  for (int j = 0; j < W; ++j) srcs[j] = slot(x, (r + 1 + j) % W, which) + off_elems * es;
+  for (int j = 0; j < W; ++j) srcs[j] = by_rank[(r + 1 + j) % W] + off_elems * es;
+  double tk = us_now();
   if (pgk_reduce_multi(out, srcs, W, len, dt, op, (void *)im->red)) {
     pg_set_error("xgmi: %s", pgk_last_error());
     return -1;
   }
+  if (pg_stream_wait(im->red)) return -1;
+  im->stats.kernel_us += us_now() - tk;
   im->stats.reduce_launches += 1;
   im->stats.reduce_elems += (int64_t)len * (W - 1);
   im->stats.bytes_recv += (int64_t)(len * es) * (W - 1);
   return 0;
 }
 
+static int overlaps(const void *a, size_t na, const void *b, size_t nb) {
+  const char *x = (const char *)a, *y = (const char *)b;
+  return na && nb && x < y + nb && y < x + na;
+}
+
 int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
-  struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
   if (ensure(pg, bytes)) return -1;
-  int rd = is_dev(recvbuf);
-  char *xs;
-  if (publish(pg, sendbuf, bytes, is_dev(sendbuf), &xs)) return -1;
+  int rd = is_dev(recvbuf), zc, fail;
+  const char *by_rank[16];
+  if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, len * es), by_rank,
+                   &zc, &fail))
+    return -1;
   void *out = recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, len * es)) return -1;
     out = im->dout;
   }
-  double tk = us_now();
-  if (fold_block(pg, out, (int)(x->gen & 1), off, len, dt, op)) return -1;
-  if (pg_stream_wait(im->red)) return -1;
-  im->stats.kernel_us += us_now() - tk;
+  if (!fail && fold_block(pg, out, by_rank, off, len, dt, op)) fail = 1;
+  if (finish(pg, zc, fail)) return -1;
   if (!rd && len && pg_copy_parallel(recvbuf, out, len * es)) return -1;
-  x->gen++;
   return 0;
 }
 
-/* Gather: block q (elements [off(q), off(q)+len(q)) of slot `which` of rank
- * q) into full + off(q), every rank's range in one launch (pgk_gather). */
-static int gather(struct pg *pg, char *full, int which, int count, int uniform, int dt) {
+/* Gather block q of every rank (bases by_rank[q], uniform: blocks of `count`
+ * at base + 0; else the reduce-scatter partition at base + off(q)) into
+ * full + off(q), one launch (pgk_gather). */
+static int gather(struct pg *pg, char *full, const char *const *by_rank, int count, int uniform, int dt) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
-  struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt);
   void *dst[16];
   const void *src[16];
-  size_t bytes[16];
+  size_t nb[16];
   int k = 0;
   for (int q = 0; q < pg->world_size; ++q) {
     size_t off, len;
@@ -251,33 +398,36 @@ static int gather(struct pg *pg, char *full, int which, int count, int uniform, 
     else pg_block_range(count, pg->world_size, q, &off, &len);
     if (!len) continue;
     dst[k] = full + off * es;
-    src[k] = slot(x, q, which) + (uniform ? 0 : off * es);
-    bytes[k] = len * es;
+    src[k] = by_rank[q] + (uniform ? 0 : off * es);
+    nb[k] = len * es;
     ++k;
   }
-  if (pgk_gather(dst, src, bytes, k, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
+  double tk = us_now();
+  if (pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
   if (pg_stream_wait(im->red)) return -1;
+  im->stats.kernel_us += us_now() - tk;
   return 0;
 }
 
 int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
-  struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), slot_bytes = (size_t)count * es, total = slot_bytes * (size_t)pg->world_size;
   if (ensure(pg, slot_bytes)) return -1;
-  int rd = is_dev(recvbuf);
+  int rd = is_dev(recvbuf), zc, fail;
   const void *mine = sendbuf ? sendbuf : (const char *)recvbuf + (size_t)pg->rank * slot_bytes;
-  char *xs;
-  if (publish(pg, mine, slot_bytes, sendbuf ? is_dev(sendbuf) : rd, &xs)) return -1;
+  const char *by_rank[16];
+  if (share_inputs(pg, mine, slot_bytes, sendbuf ? is_dev(sendbuf) : rd, overlaps(mine, slot_bytes, recvbuf, total),
+                   by_rank, &zc, &fail))
+    return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
     full = (char *)im->dout;
   }
-  if (gather(pg, full, (int)(x->gen & 1), count, 1, dt)) return -1;
+  if (!fail && gather(pg, full, by_rank, count, 1, dt)) fail = 1;
+  if (finish(pg, zc, fail)) return -1;
   if (!rd && total && pg_copy_parallel(recvbuf, full, total)) return -1;
   im->stats.bytes_recv += (int64_t)(total - slot_bytes);
-  x->gen++;
   return 0;
 }
 
@@ -287,48 +437,42 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
   if (ensure(pg, bytes)) return -1;
-  int rd = is_dev(recvbuf), which = (int)(x->gen & 1);
-  char *xs;
-  if (publish(pg, sendbuf, bytes, is_dev(sendbuf), &xs)) return -1;
-  if (bytes <= x->oneshot_max) {
-    /* small message: every rank folds the whole vector itself, each block in
-     * its ring order -- one launch, no second barrier */
-    char *full = (char *)recvbuf;
-    if (!rd) {
-      if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
-      full = (char *)im->dout;
-    }
-    const void *srcs[16];
-    for (int q = 0; q < pg->world_size; ++q) srcs[q] = slot(x, q, which);
-    size_t blk = ((size_t)count + (size_t)pg->world_size - 1) / (size_t)pg->world_size;
-    double tk = us_now();
-    if (count && pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, dt, op, (void *)im->red)) {
-      pg_set_error("xgmi: %s", pgk_last_error());
-      return -1;
-    }
-    if (pg_stream_wait(im->red)) return -1;
-    im->stats.kernel_us += us_now() - tk;
-    if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
-    x->gen++;
-    return 0;
-  }
-  double tk = us_now();
-  /* my block of the result goes to R[which] so that every rank can gather it */
-  if (fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, which, off, len, dt, op)) return -1;
-  if (pg_stream_wait(im->red)) return -1;
-  double tb = us_now();
-  im->stats.kernel_us += tb - tk;
-  if (barrier(pg)) return -1;
-  im->stats.barrier_us += us_now() - tb;
+  int rd = is_dev(recvbuf), which = (int)(x->gen & 1), zc, fail;
+  const char *by_rank[16];
+  if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, bytes), by_rank, &zc,
+                   &fail))
+    return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
     full = (char *)im->dout;
   }
-  double tg = us_now();
-  if (gather(pg, full, 2 + which, count, 0, dt)) return -1;
-  im->stats.kernel_us += us_now() - tg;
+  if (bytes <= x->oneshot_max) {
+    /* small message: every rank folds the whole vector itself, each block in
+     * its ring order -- one launch, no second barrier */
+    if (!fail && count) {
+      const void *srcs[16];
+      for (int q = 0; q < pg->world_size; ++q) srcs[q] = by_rank[q];
+      size_t blk = ((size_t)count + (size_t)pg->world_size - 1) / (size_t)pg->world_size;
+      double tk = us_now();
+      if (pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, dt, op, (void *)im->red) ||
+          pg_stream_wait(im->red)) {
+        pg_set_error("xgmi: %s", pgk_last_error());
+        fail = 1;
+      }
+      im->stats.kernel_us += us_now() - tk;
+    }
+  } else {
+    /* my block of the result goes to R[which] so that every rank can gather it */
+    if (!fail && fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, by_rank, off, len, dt, op)) fail = 1;
+    double tb = us_now();
+    if (barrier(pg)) return -1;
+    im->stats.barrier_us += us_now() - tb;
+    const char *res_by_rank[16];
+    for (int q = 0; q < pg->world_size; ++q) res_by_rank[q] = slot(x, q, 2 + which);
+    if (!fail && gather(pg, full, res_by_rank, count, 0, dt)) fail = 1;
+  }
+  if (finish(pg, zc, fail)) return -1;
   if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
-  x->gen++;
   return 0;
 }

@@ -21,6 +21,9 @@ CASES = [  # coll, dt, op, count, on_dev, in_place
     ("ar", 1, 0, 100003, True, False), ("ar", 0, 1, 999, False, False), ("ar", 1, 1, 4096, True, True),
     ("ar", 0, 0, 7, False, True), ("rs", 1, 0, 5000, True, False), ("ar", 1, 0, 300001, True, False),
     ("ar", 0, 1, 524288, False, True),
+    # "mixed": even ranks pass device buffers, odd ranks host buffers -> every
+    # rank must agree to fall back from zero-copy to the slot copy
+    ("rs", 1, 0, 77777, "mixed", False), ("ar", 0, 0, 300000, "mixed", False), ("ag", 1, 0, 999, "mixed", False),
 ]
 
 
@@ -32,9 +35,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, oneshot_max):
+def _worker(rank, world, port, q, oneshot_max, zero_copy="1"):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max))
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max), PG_XGMI_ZERO_COPY=zero_copy)
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -56,6 +59,8 @@ def _worker(rank, world, port, q, oneshot_max):
         assert (hd.rank, hd.world_size, hd.transport) == (rank, world, pgamd.PG_TRANSPORT_XGMI)
         NP = {0: np.int32, 1: np.float64}
         for i, (coll, dt, op, count, on_dev, in_place) in enumerate(CASES):
+            if on_dev == "mixed":
+                on_dev = rank % 2 == 0
             xs = [orc.fill(count, dt, op, 700 + 13 * i + r) for r in range(world)]
             if coll == "rs":
                 want = orc.ring_reduce_scatter(xs, dt, op)[rank]
@@ -94,16 +99,18 @@ def _worker(rank, world, port, q, oneshot_max):
     q.put((rank, fails))
 
 
-@pytest.mark.parametrize("world,oneshot_max", [(2, 1 << 20), (3, 1 << 20), (4, 1 << 20), (8, 1 << 20),
-                                               (2, 0), (5, 0), (4, 1 << 40)])
-def test_xgmi_multiprocess(gpu, world, oneshot_max):
+@pytest.mark.parametrize("world,oneshot_max,zero_copy", [(2, 1 << 20, "1"), (3, 1 << 20, "1"), (4, 1 << 20, "1"),
+                                                         (8, 1 << 20, "1"), (2, 0, "1"), (5, 0, "1"),
+                                                         (4, 1 << 40, "1"), (3, 1 << 20, "0"), (4, 0, "0")])
+def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy):
     """oneshot_max selects the all-reduce form: 0 = always reduce-scatter +
-    gather, 2^40 = always the one-shot fold, 1 MiB = the default split."""
+    gather, 2^40 = always the one-shot fold, 1 MiB = the default split.
+    zero_copy "0" forces the slot copy for every input."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max, zero_copy)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
