@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--sizes", default="", help="comma-separated byte sizes (default: 4 KiB .. 1 GiB)")
+    ap.add_argument("--ab", action="store_true", help="only the one-shot nt shapes (A/B of block shape)")
     args = ap.parse_args()
     lib = pgamd.load()
     torch.cuda.set_device(0)
@@ -55,6 +57,10 @@ def main():
         sizes = [1 << 20, 1 << 26, 1 << 28]
         bpcs = [0, 8]
         shapes = [(256, 4), (512, 2)]
+    if args.sizes:
+        sizes = [int(x) for x in args.sizes.split(",")]
+    if args.ab:
+        bpcs, nts = [0], [1]
     variants = [(b, nt, sh_) for b in bpcs for nt in nts for sh_ in shapes]
     rows = []
     out = pathlib.Path(args.out)
