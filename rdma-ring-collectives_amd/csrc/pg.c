@@ -85,7 +85,7 @@ int pg_ensure(void **buf, size_t *cap, size_t bytes) {
 
 /* HIP device or managed memory?  Anything else is treated as host memory and
  * staged through HBM. */
-static int is_device_ptr(const void *p) {
+int pg_is_device_ptr(const void *p) {
   if (!p) return 0;
   hipPointerAttribute_t a;
   memset(&a, 0, sizeof(a));
@@ -96,7 +96,7 @@ static int is_device_ptr(const void *p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
 }
 
-static int ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+int pg_ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
   const char *x = (const char *)a, *y = (const char *)b;
   return na && nb && x < y + nb && y < x + na;
 }
@@ -159,14 +159,14 @@ int pg_copy_parallel(void *dst, const void *src, size_t bytes) {
 
 static int copy_any(void *dst, const void *src, size_t bytes) {
   if (!bytes || dst == src) return 0;
-  int dd = is_device_ptr(dst), sd = is_device_ptr(src);
+  int dd = pg_is_device_ptr(dst), sd = pg_is_device_ptr(src);
   if (!dd && !sd) { memmove(dst, src, bytes); return 0; }
   if (dd != sd) return pg_copy_parallel(dst, src, bytes);      /* crosses PCIe */
   PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
   return 0;
 }
 
-static int timed_copy(void *dst, const void *src, size_t bytes, double *acc_us) {
+int pg_timed_copy(void *dst, const void *src, size_t bytes, double *acc_us) {
   double t = now_us();
   int rc = copy_any(dst, src, bytes);
   *acc_us += now_us() - t;
@@ -188,6 +188,8 @@ int pg_impl_create(struct pg *pg) {
   PG_CHECK_HIP(hipEventCreateWithFlags(&im->join_ev, hipEventDisableTiming));
   PG_CHECK_HIP(hipEventCreate(&im->t0));
   PG_CHECK_HIP(hipEventCreate(&im->t1));
+  const char *e = getenv("PG_EAGER_ONESHOT");
+  im->eager_oneshot = !(e && *e && atoi(e) == 0);
   return 0;
 }
 
@@ -213,6 +215,7 @@ void pg_impl_destroy(struct pg *pg) {
   for (int i = 0; i < 2; ++i) if (im->stage[i]) hipFree(im->stage[i]);
   if (im->dsrc) hipFree(im->dsrc);
   if (im->dout) hipFree(im->dout);
+  if (im->ebuf) hipFree(im->ebuf);
   free(im->steps);
   free(im);
   pg->impl = NULL;
@@ -360,7 +363,7 @@ static int upload_block(struct pg *pg, struct stage_ctx *c, int b) {
   size_t es = pg_elem_size(c->dt), off, len;
   stage_block(c, pg->world_size, b, &off, &len);
   c->up[b] = 1;
-  return len ? timed_copy(c->dev_src + off * es, c->host_src + off * es, len * es, c->h2d_us) : 0;
+  return len ? pg_timed_copy(c->dev_src + off * es, c->host_src + off * es, len * es, c->h2d_us) : 0;
 }
 
 /* reduce-scatter rounds: round k reads source blocks r-1 (k = 0, sent) and r-2-k */
@@ -389,7 +392,7 @@ static int ag_download_hook(struct pg_impl *im, void *ctx, int k) {
     int b = ((pg->rank - j - 1) % pg->world_size + pg->world_size) % pg->world_size;
     size_t off, len;
     stage_block(c, pg->world_size, b, &off, &len);
-    if (len && timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us)) return -1;
+    if (len && pg_timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us)) return -1;
   }
   c->next_dl = k;
   return 0;
@@ -401,7 +404,7 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t es = pg_elem_size(dt), boff, blen;
   pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
-  int sd = is_device_ptr(sendbuf), rd = is_device_ptr(recvbuf);
+  int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
   if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());   /* caller's producers */
 
   void *src = sendbuf;
@@ -421,13 +424,13 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
       sc.up = up;
       sc.h2d_us = &im->stats.h2d_us;
       sc.d2h_us = &im->stats.d2h_us;
-    } else if (timed_copy(im->dsrc, sendbuf, (size_t)count * es, &im->stats.h2d_us)) {
+    } else if (pg_timed_copy(im->dsrc, sendbuf, (size_t)count * es, &im->stats.h2d_us)) {
       return -1;
     }
   }
   void *out = recvbuf;
   int post_copy = 0;
-  if (!rd || ranges_overlap(recvbuf, blen * es, src, (size_t)count * es)) {
+  if (!rd || pg_ranges_overlap(recvbuf, blen * es, src, (size_t)count * es)) {
     if (pg_ensure(&im->dout, &im->dout_cap, blen * es)) return -1;
     out = im->dout;
     post_copy = 1;
@@ -440,7 +443,7 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
   if (pg_exec_plan(im, im->steps, n, bufs, dt, op, lazy ? rs_upload_hook : NULL, &sc)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
   if (sync_ring(im, 1)) return -1;
-  if (post_copy && timed_copy(recvbuf, out, blen * es, &im->stats.d2h_us)) return -1;
+  if (post_copy && pg_timed_copy(recvbuf, out, blen * es, &im->stats.d2h_us)) return -1;
   return 0;
 }
 
@@ -463,24 +466,24 @@ static int loopback_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, 
       return -1;
     }
   }
-  int sd = is_device_ptr(sendbuf), rd = is_device_ptr(recvbuf);
+  int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
   if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());
   char *s, *d;
   if (sendbuf == recvbuf) {
     if (rd) s = d = (char *)recvbuf;
     else {
-      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || pg_timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
       s = d = (char *)im->dout;
     }
   } else {
     if (sd) s = (char *)sendbuf;
     else {
-      if (pg_ensure(&im->dsrc, &im->dsrc_cap, bytes) || timed_copy(im->dsrc, sendbuf, bytes, &im->stats.h2d_us)) return -1;
+      if (pg_ensure(&im->dsrc, &im->dsrc_cap, bytes) || pg_timed_copy(im->dsrc, sendbuf, bytes, &im->stats.h2d_us)) return -1;
       s = (char *)im->dsrc;
     }
     if (rd) d = (char *)recvbuf;
     else {
-      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
+      if (pg_ensure(&im->dout, &im->dout_cap, bytes) || pg_timed_copy(im->dout, recvbuf, bytes, &im->stats.h2d_us)) return -1;
       d = (char *)im->dout;
     }
   }
@@ -502,7 +505,7 @@ static int loopback_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, 
   PG_CHECK_HIP(hipStreamSynchronize(im->red));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us = (double)ms * 1e3;
-  if (!rd && timed_copy(recvbuf, d, bytes, &im->stats.d2h_us)) return -1;
+  if (!rd && pg_timed_copy(recvbuf, d, bytes, &im->stats.d2h_us)) return -1;
   return 0;
 }
 
@@ -525,6 +528,8 @@ int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype
     rc = loopback_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else if (pg->transport == PG_TRANSPORT_XGMI)
     rc = pg_xgmi_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_eager_applies(pg, count, datatype))
+    rc = pg_eager_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;
@@ -536,7 +541,7 @@ int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype
 static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)pg->world_size;
-  int rd = is_device_ptr(recvbuf), sd = sendbuf && is_device_ptr(sendbuf);
+  int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
   if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
   char *full = (char *)recvbuf;
   if (!rd) {
@@ -545,9 +550,9 @@ static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   }
   char *own = full + (size_t)pg->rank * slot;
   if (sendbuf) {
-    if ((char *)sendbuf != own && timed_copy(own, sendbuf, slot, sd ? &im->stats.ring_us : &im->stats.h2d_us)) return -1;
+    if ((char *)sendbuf != own && pg_timed_copy(own, sendbuf, slot, sd ? &im->stats.ring_us : &im->stats.h2d_us)) return -1;
   } else if (!rd) {
-    if (timed_copy(own, (char *)recvbuf + (size_t)pg->rank * slot, slot, &im->stats.h2d_us)) return -1;
+    if (pg_timed_copy(own, (char *)recvbuf + (size_t)pg->rank * slot, slot, &im->stats.h2d_us)) return -1;
   }
   int n = plan_into(im, 0, count, dt, 0, 1);
   if (n < 0) return -1;
@@ -566,7 +571,7 @@ static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   if (sync_ring(im, 1)) return -1;
   /* the hook downloaded every received block as its round completed; this
    * rank's own block is still only on the device */
-  if (!rd && timed_copy((char *)recvbuf + (size_t)pg->rank * slot, own, slot, &im->stats.d2h_us)) return -1;
+  if (!rd && pg_timed_copy((char *)recvbuf + (size_t)pg->rank * slot, own, slot, &im->stats.d2h_us)) return -1;
   return 0;
 }
 
@@ -576,14 +581,14 @@ static int loopback_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int 
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   int W = pg->world_size, r = pg->rank;
   size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)W;
-  int rd = is_device_ptr(recvbuf), sd = sendbuf && is_device_ptr(sendbuf);
+  int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
   if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
   char *full = (char *)recvbuf;
   if (!rd) {
-    if (pg_ensure(&im->dout, &im->dout_cap, total) || timed_copy(im->dout, recvbuf, total, &im->stats.h2d_us)) return -1;
+    if (pg_ensure(&im->dout, &im->dout_cap, total) || pg_timed_copy(im->dout, recvbuf, total, &im->stats.h2d_us)) return -1;
     full = (char *)im->dout;
   }
-  if (sendbuf && timed_copy(full + (size_t)r * slot, sendbuf, slot, &im->stats.h2d_us)) return -1;
+  if (sendbuf && pg_timed_copy(full + (size_t)r * slot, sendbuf, slot, &im->stats.h2d_us)) return -1;
   for (int k = 0; k + 1 < W; ++k) {
     int s = ((r - k) % W + W) % W, d = ((r - k - 1) % W + W) % W;
     if (pgk_reduce(full + (size_t)d * slot, full + (size_t)s * slot, (size_t)count, dt, PGK_OP_SUM,
@@ -594,7 +599,7 @@ static int loopback_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int 
     im->stats.reduce_launches++;
   }
   PG_CHECK_HIP(hipStreamSynchronize(im->red));
-  if (!rd && timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
+  if (!rd && pg_timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
   return 0;
 }
 
@@ -615,6 +620,8 @@ int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, vo
     rc = loopback_all_gather(pg, sendbuf, recvbuf, count, datatype);
   else if (pg->transport == PG_TRANSPORT_XGMI)
     rc = pg_xgmi_all_gather(pg, sendbuf, recvbuf, count, datatype);
+  else if (pg_eager_applies(pg, count, datatype))
+    rc = pg_eager_all_gather(pg, sendbuf, recvbuf, count, datatype);
   else
     rc = ring_all_gather(pg, sendbuf, recvbuf, count, datatype);
   im->stats.wall_us = now_us() - t;
@@ -630,7 +637,7 @@ static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, boff, blen;
   pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
-  int rd = is_device_ptr(recvbuf), sd = is_device_ptr(sendbuf);
+  int rd = pg_is_device_ptr(recvbuf), sd = pg_is_device_ptr(sendbuf);
   if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
   char *work = (char *)recvbuf;
   if (!rd) {
@@ -641,13 +648,13 @@ static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int coun
    * -- block by block between the reduce-scatter rounds */
   const void *host_in = NULL;
   if (sendbuf != recvbuf) {
-    if (sd) { if (timed_copy(work, sendbuf, bytes, &im->stats.ring_us)) return -1; }
+    if (sd) { if (pg_timed_copy(work, sendbuf, bytes, &im->stats.ring_us)) return -1; }
     else host_in = sendbuf;
   } else if (!rd) {
     host_in = recvbuf;
   }
   if (host_in && pg->world_size > 64) {
-    if (timed_copy(work, host_in, bytes, &im->stats.h2d_us)) return -1;
+    if (pg_timed_copy(work, host_in, bytes, &im->stats.h2d_us)) return -1;
     host_in = NULL;
   }
   if (ensure_stage(im, count, dt)) return -1;
@@ -679,7 +686,7 @@ static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   if (sync_ring(im, 1)) return -1;
   /* received blocks were downloaded round by round; this rank's own block
    * (reduced here) is still only on the device */
-  if (!rd && blen && timed_copy((char *)recvbuf + boff * es, work + boff * es, blen * es, &im->stats.d2h_us))
+  if (!rd && blen && pg_timed_copy((char *)recvbuf + boff * es, work + boff * es, blen * es, &im->stats.d2h_us))
     return -1;
   return 0;
 }
@@ -709,6 +716,8 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
     rc = -1;
   } else if (pg->transport == PG_TRANSPORT_XGMI)
     rc = pg_xgmi_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_eager_applies(pg, count, datatype))
+    rc = pg_eager_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;

@@ -67,6 +67,8 @@ struct pg_impl {
   void *stage[2];  size_t stage_cap;
   void *dsrc;      size_t dsrc_cap;   /* device copy of a host sendbuf        */
   void *dout;      size_t dout_cap;   /* device result / full buffer          */
+  void *ebuf;      size_t ebuf_cap;   /* eager one-shot gather area (pg_eager.c) */
+  int eager_oneshot;          /* PG_EAGER_ONESHOT, default 1                  */
 
   struct pg_step *steps; int steps_cap;
   int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */
@@ -81,6 +83,15 @@ int pg_copy_parallel(void *dst, const void *src, size_t bytes);  /* host<->devic
 int pg_impl_create(struct pg *pg);                        /* streams/events */
 void pg_impl_destroy(struct pg *pg);
 size_t pg_elem_size(int dt);
+int pg_is_device_ptr(const void *p);                      /* HIP device/managed memory? */
+int pg_ranges_overlap(const void *a, size_t na, const void *b, size_t nb);
+int pg_timed_copy(void *dst, const void *src, size_t bytes, double *acc_us);  /* any direction */
+
+/* pg_eager.c: one group + one launch for messages <= eager_max (P2P transports) */
+int pg_eager_applies(const struct pg *pg, int count, int dt);
+int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
+int pg_eager_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt);
+int pg_eager_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
 
 /* pg_exec.c: run `n` steps; bufs[] indexed by PG_BUF_*.  If `hook` is set it
  * is called on the host before the first batch of each round k (and once with

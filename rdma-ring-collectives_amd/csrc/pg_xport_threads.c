@@ -30,7 +30,7 @@ struct sim_msg {
   struct sim_msg *next;
 };
 
-struct sim_chan {              /* edge r -> r+1 */
+struct sim_chan {              /* edge src -> dst: chan[src * world + dst] */
   struct sim_msg *head, *tail;
   long pushed, acked;
 };
@@ -43,7 +43,7 @@ struct sim_hub {
   struct sim_chan *chan;
 };
 
-struct sim_io { void *buf; size_t bytes; };
+struct sim_io { void *buf; size_t bytes; int peer; };
 
 struct sim_rank {
   struct sim_hub *hub;
@@ -66,7 +66,7 @@ static int th_group_start(struct pg_impl *im) {
   return 0;
 }
 
-static int push_io(struct sim_io **arr, int *n, int *cap, void *buf, size_t bytes) {
+static int push_io(struct sim_io **arr, int *n, int *cap, void *buf, size_t bytes, int peer) {
   if (*n == *cap) {
     int c = *cap ? *cap * 2 : 16;
     struct sim_io *a = (struct sim_io *)realloc(*arr, sizeof(**arr) * (size_t)c);
@@ -76,28 +76,29 @@ static int push_io(struct sim_io **arr, int *n, int *cap, void *buf, size_t byte
   }
   (*arr)[*n].buf = buf;
   (*arr)[*n].bytes = bytes;
+  (*arr)[*n].peer = peer;
   ++*n;
   return 0;
 }
 
 static int th_send(struct pg_impl *im, const void *buf, size_t bytes, int peer, hipStream_t s) {
-  (void)peer; (void)s;
+  (void)s;
   struct sim_rank *sr = (struct sim_rank *)im->xctx;
-  if (push_io(&sr->sends, &sr->n_send, &sr->cap_send, (void *)buf, bytes)) { pg_set_error("sim: oom"); return -1; }
+  if (push_io(&sr->sends, &sr->n_send, &sr->cap_send, (void *)buf, bytes, peer)) { pg_set_error("sim: oom"); return -1; }
   return 0;
 }
 
 static int th_recv(struct pg_impl *im, void *buf, size_t bytes, int peer, hipStream_t s) {
-  (void)peer; (void)s;
+  (void)s;
   struct sim_rank *sr = (struct sim_rank *)im->xctx;
-  if (push_io(&sr->recvs, &sr->n_recv, &sr->cap_recv, buf, bytes)) { pg_set_error("sim: oom"); return -1; }
+  if (push_io(&sr->recvs, &sr->n_recv, &sr->cap_recv, buf, bytes, peer)) { pg_set_error("sim: oom"); return -1; }
   return 0;
 }
 
 static int th_group_end(struct pg_impl *im, hipStream_t s) {
   struct sim_rank *sr = (struct sim_rank *)im->xctx;
   struct sim_hub *h = sr->hub;
-  const int r = im->pg->rank, left = (r - 1 + h->world) % h->world;
+  const int r = im->pg->rank, W = h->world;
   /* everything enqueued before the group (incl. waits on reduces) is done */
   PG_CHECK_HIP(hipStreamSynchronize(s));
 
@@ -107,7 +108,7 @@ static int th_group_end(struct pg_impl *im, hipStream_t s) {
     if (!m) { h->abort = 1; pthread_cond_broadcast(&h->cv); pthread_mutex_unlock(&h->mu); pg_set_error("sim: oom"); return -1; }
     m->buf = sr->sends[i].buf;
     m->bytes = sr->sends[i].bytes;
-    struct sim_chan *c = &h->chan[r];
+    struct sim_chan *c = &h->chan[r * W + sr->sends[i].peer];
     if (c->tail) c->tail->next = m; else c->head = m;
     c->tail = m;
     c->pushed++;
@@ -116,17 +117,18 @@ static int th_group_end(struct pg_impl *im, hipStream_t s) {
   pthread_mutex_unlock(&h->mu);
 
   for (int i = 0; i < sr->n_recv; ++i) {
+    const int from = sr->recvs[i].peer;
     pthread_mutex_lock(&h->mu);
-    struct sim_chan *c = &h->chan[left];
+    struct sim_chan *c = &h->chan[from * W + r];
     while (!c->head) {
-      if (hub_wait(h)) { pthread_mutex_unlock(&h->mu); pg_set_error("sim: rank %d timed out waiting for rank %d", r, left); return -1; }
+      if (hub_wait(h)) { pthread_mutex_unlock(&h->mu); pg_set_error("sim: rank %d timed out waiting for rank %d", r, from); return -1; }
     }
     struct sim_msg *m = c->head;
     c->head = m->next;
     if (!c->head) c->tail = NULL;
     pthread_mutex_unlock(&h->mu);
     if (m->bytes != sr->recvs[i].bytes) {
-      pg_set_error("sim: rank %d expected %zu bytes from rank %d, got %zu", r, sr->recvs[i].bytes, left, m->bytes);
+      pg_set_error("sim: rank %d expected %zu bytes from rank %d, got %zu", r, sr->recvs[i].bytes, from, m->bytes);
       free(m);
       pthread_mutex_lock(&h->mu); h->abort = 1; pthread_cond_broadcast(&h->cv); pthread_mutex_unlock(&h->mu);
       return -1;
@@ -138,10 +140,13 @@ static int th_group_end(struct pg_impl *im, hipStream_t s) {
   PG_CHECK_HIP(hipStreamSynchronize(s));
 
   pthread_mutex_lock(&h->mu);
-  h->chan[left].acked += sr->n_recv;
+  for (int i = 0; i < sr->n_recv; ++i) h->chan[sr->recvs[i].peer * W + r].acked += 1;
   pthread_cond_broadcast(&h->cv);
-  while (h->chan[r].acked < h->chan[r].pushed) {
-    if (hub_wait(h)) { pthread_mutex_unlock(&h->mu); pg_set_error("sim: rank %d: sends never consumed", r); return -1; }
+  for (int i = 0; i < sr->n_send; ++i) {
+    struct sim_chan *c = &h->chan[r * W + sr->sends[i].peer];
+    while (c->acked < c->pushed) {
+      if (hub_wait(h)) { pthread_mutex_unlock(&h->mu); pg_set_error("sim: rank %d: sends never consumed", r); return -1; }
+    }
   }
   pthread_mutex_unlock(&h->mu);
   return 0;
@@ -208,7 +213,7 @@ int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbuf
   hub.world = world;
   pthread_mutex_init(&hub.mu, NULL);
   pthread_cond_init(&hub.cv, NULL);
-  hub.chan = (struct sim_chan *)calloc((size_t)world, sizeof(struct sim_chan));
+  hub.chan = (struct sim_chan *)calloc((size_t)world * (size_t)world, sizeof(struct sim_chan));
   struct sim_job *jobs = (struct sim_job *)calloc((size_t)world, sizeof(struct sim_job));
   pthread_t *tid = (pthread_t *)calloc((size_t)world, sizeof(pthread_t));
   int rc = -1, started = 0;
@@ -243,7 +248,7 @@ int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbuf
 out:
   for (int r = 0; jobs && r < world; ++r) if (jobs[r].pg) pg_close(jobs[r].pg);
   if (hub.chan) {
-    for (int r = 0; r < world; ++r) {
+    for (int r = 0; r < world * world; ++r) {
       struct sim_msg *m = hub.chan[r].head;
       while (m) { struct sim_msg *n = m->next; free(m); m = n; }
     }

@@ -260,3 +260,57 @@ def test_ring_large_device_resident(gpu, lib, oracle):
     for r in range(world):
         assert got[r].tobytes() == want[r].tobytes()
     torch.cuda.empty_cache()
+
+
+# Eager one-shot (csrc/pg_eager.c): messages <= eager_max bytes per rank use one
+# transport group + one fold launch; the fold keeps the ring's per-block order,
+# so the results must equal the ring oracle bit for bit.
+EAGER_CASES = [  # world, dt, op, count   (eager_max = 4096 bytes)
+    (2, 1, 0, 1), (3, 0, 1, 7), (4, 1, 0, 512), (8, 1, 1, 5), (8, 0, 0, 1024),
+    (16, 1, 0, 300), (5, 1, 0, 511), (6, 0, 1, 2), (17, 1, 0, 100),   # W=17: ring fallback
+]
+
+
+@pytest.mark.parametrize("case", EAGER_CASES)
+def test_eager_oneshot_sim(gpu, lib, oracle, case):
+    world, dt, op, count = case
+    xs = [oracle.fill(count, dt, op, 5000 + 11 * r + count) for r in range(world)]
+    want_rs = oracle.ring_reduce_scatter(xs, dt, op)
+    want_ar = oracle.ring_all_reduce(xs, dt, op)
+    want_ag = oracle.ring_all_gather(xs, dt)
+    for on_dev in (True, False):
+        recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want_rs]
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, 0, 4096, 4, on_dev)
+        for r in range(world):
+            assert got[r][:want_rs[r].size].tobytes() == want_rs[r].tobytes(), (case, "rs", r, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, NP[dt]) for _ in xs],
+                  count, dt, op, 0, 4096, 4, on_dev)
+        for r in range(world):
+            assert got[r].tobytes() == want_ar[r].tobytes(), (case, "ar", r, on_dev)
+        # in place
+        R = [to_dev(gpu, x) for x in xs] if on_dev else [x.copy() for x in xs]
+        ps = (ctypes.c_void_p * world)(*[(ptr(r) if on_dev else r.ctypes.data) for r in R])
+        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, 0, 4096, 4) == 0, \
+            pgamd.last_error()
+        for r in range(world):
+            g = to_host(gpu, R[r]) if on_dev else R[r]
+            assert g.tobytes() == want_ar[r].tobytes(), (case, "ar-inplace", r, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, [np.zeros(count * world, NP[dt]) for _ in xs],
+                  count, dt, 0, 0, 4096, 4, on_dev)
+        for r in range(world):
+            assert got[r].tobytes() == want_ag[r].tobytes(), (case, "ag", r, on_dev)
+
+
+def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch):
+    """Same inputs through the one-shot and through the W-1 round ring
+    (PG_EAGER_ONESHOT=0): byte-identical outputs, doubles included."""
+    world, count = 8, 509
+    for dt, op in ((1, 0), (1, 1), (0, 0), (0, 1)):
+        xs = [oracle.fill(count, dt, op, 6000 + r) for r in range(world)]
+        outs = []
+        for flag in ("1", "0"):
+            monkeypatch.setenv("PG_EAGER_ONESHOT", flag)
+            outs.append(sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, NP[dt]) for _ in xs],
+                            count, dt, op, 0, 4096, 4, True))
+        for a, b in zip(*outs):
+            assert a.tobytes() == b.tobytes(), (dt, op)
