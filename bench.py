@@ -399,8 +399,15 @@ def ring_leg(lib, args, rank, world, transport):
                     t = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
                     good = bool(torch.equal(ov[:l5], _expected_block(cnt, o5, l5, world, dt5, pgamd.OP_PROD)))
                     good = sum_over_ranks(1.0 if good else 0.0, world) == world
-                    cfg5.append({"dtype": "f64" if dt5 == pgamd.DT_DOUBLE else "i32", "count": cnt,
-                                 "bytes": cnt * pgamd.ELEM_SIZE[dt5], "time_us": round(t * 1e6, 1), "ok": good})
+                    row = {"dtype": "f64" if dt5 == pgamd.DT_DOUBLE else "i32", "count": cnt,
+                           "bytes": cnt * pgamd.ELEM_SIZE[dt5], "time_us": round(t * 1e6, 1), "ok": good}
+                    if cnt == small and transport == "rccl":
+                        # eager one-shot (default) vs the W-1 round ring: eager_max = 0 disables it
+                        hd.eager_max = 0
+                        tr = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
+                        hd.eager_max = 4096
+                        row["time_us_ring_rounds"] = round(tr * 1e6, 1)
+                    cfg5.append(row)
                     del xv, ov
                     torch.cuda.empty_cache()
             res["config5_prod_mixed"] = cfg5
