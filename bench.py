@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    ap.add_argument("--cpu-procs", type=int, default=8,
+                    help="CPU baseline: also time this many concurrent reference processes (0/1: skip)")
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
@@ -98,6 +100,16 @@ def max_over_ranks(x: float, world: int) -> float:
     t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_over_ranks(x: float, rank: int, world: int) -> list:
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    t = torch.zeros(world, dtype=torch.float64)
+    t[rank] = x
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t]
 
 
 def sum_over_ranks(x: float, world: int) -> float:
@@ -170,8 +182,10 @@ def cpu_baseline(args):
     except RuntimeError:
         impl, kind = Oracle(), "port"
     orc = Oracle()
+    orig_aff = None
     try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+        orig_aff = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {sorted(orig_aff)[0]})
     except (AttributeError, OSError):
         pass
     n = N_ELEMS                                   # the same 256 MiB chunk
@@ -191,7 +205,24 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
+    if orig_aff:
+        try:
+            os.sched_setaffinity(0, orig_aff)     # the rest of the bench (and the child below) unpinned
+        except OSError:
+            pass
+    del d, s
+    concurrent = None
+    if args.cpu_procs > 1:       # W ranks of the reference at once, in a fresh child process
+        import subprocess
+        try:
+            r = subprocess.run([sys.executable, "-m", "oracle.cpu_concurrent", "--procs", str(args.cpu_procs),
+                                "--seconds", "5"], cwd=str(ROOT), capture_output=True, text=True, timeout=300)
+            concurrent = (json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0
+                          else {"error": r.stderr.strip()[-300:]})
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the primary line
+            concurrent = {"error": f"{type(e).__name__}: {e}"}
     return {"value": round(gibs, 3), "unit": "GiB/s (3*n*8 B traffic)", "cores": 1, "kind": kind,
+            "concurrent": concurrent,
             "payload_gibs": round(n * 8 * reps / secs / GIB, 3),
             "sample": f"{reps} x reduce_inplace(double, sum) over 256 MiB chunks, {secs:.1f} s, "
                       f"1 pinned core of {os.cpu_count()} ({cpu}); "
@@ -317,6 +348,80 @@ def _expected_block(count, off, ln, world, dt, op):
     return acc.to(tdt)
 
 
+_NCCL_GROUP = None
+
+
+def _nccl_group():
+    """An RCCL process group beside the gloo control plane (backend "nccl" is
+    RCCL on ROCm), created collectively on first use."""
+    global _NCCL_GROUP
+    if _NCCL_GROUP is None:
+        import torch.distributed as dist
+        _NCCL_GROUP = dist.new_group(backend="nccl")
+    return _NCCL_GROUP
+
+
+def native_crosscheck(lib, h, rank, world, x_full, dt_full):
+    """pg_reduce_scatter against RCCL's own reduce-scatter.
+
+    Random inputs (full-range int32, U[-1,1) doubles), 16 Mi elements per rank
+    (a multiple of W, so both libraries use the same uniform blocks).  int32:
+    bit-exact.  double: the two libraries fold the W values in different
+    orders; each sum is within g*sum|x| of the exact one (g = (W-1)u/(1-(W-1)u),
+    u = 2^-53), so |ours - rccl| <= 2*g*sum|x| element-wise, sum|x| taken from
+    an RCCL reduce-scatter of |x|.  Also times RCCL's reduce-scatter on the leg's
+    full-size input beside ours."""
+    import torch.distributed as dist
+    grp = _nccl_group()
+    n = ((1 << 24) // world) * world
+    gen = torch.Generator(device="cuda").manual_seed(777 + rank)
+    res = {}
+    for dt in (pgamd.DT_INT32, pgamd.DT_DOUBLE):
+        if dt == pgamd.DT_INT32:
+            x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=gen)
+        else:
+            x = torch.rand(n, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+        ln = n // world
+        ours = torch.empty(ln, dtype=x.dtype, device="cuda")
+        nat = torch.empty(ln, dtype=x.dtype, device="cuda")
+        torch.cuda.synchronize()
+        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), n, dt, pgamd.OP_SUM, h), "RS")
+        dist.reduce_scatter_tensor(nat, x, group=grp)
+        torch.cuda.synchronize()
+        if dt == pgamd.DT_INT32:
+            ok = bool(torch.equal(ours, nat))
+            res["i32_sum_bit_exact"] = sum_over_ranks(1.0 if ok else 0.0, world) == world
+        else:
+            sabs = torch.empty_like(nat)
+            dist.reduce_scatter_tensor(sabs, x.abs(), group=grp)
+            torch.cuda.synchronize()
+            k = (world - 1) * 2.0**-53
+            tol = 2 * k / (1 - k) * sabs
+            diff = (ours - nat).abs()
+            worst = float((diff / tol.clamp_min(1e-300)).max())
+            ident = float((ours == nat).double().mean())
+            res["f64_sum_within_tol"] = sum_over_ranks(1.0 if worst <= 1.0 else 0.0, world) == world
+            res["f64_max_diff_over_tol"] = round(max_over_ranks(worst, world), 4)
+            res["f64_bit_identical_frac"] = round(sum_over_ranks(ident, world) / world, 4)
+            res["f64_tolerance"] = "|ours - rccl| <= 2*g*sum|x|, g = (W-1)*2^-53/(1-(W-1)*2^-53)"
+        del x, ours, nat
+    # RCCL's own reduce-scatter on the leg's full input, timed like ours
+    m = (x_full.numel() // world) * world
+    nat = torch.empty(m // world, dtype=x_full.dtype, device="cuda")
+    dist.reduce_scatter_tensor(nat, x_full[:m], group=grp)         # warm
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dist.reduce_scatter_tensor(nat, x_full[:m], group=grp)
+    torch.cuda.synchronize()
+    barrier(world)
+    res["rccl_reduce_scatter_ms"] = round(max_over_ranks(time.perf_counter() - t0, world) / 3 * 1e3, 3)
+    del nat
+    torch.cuda.empty_cache()
+    return res
+
+
 def ring_leg(lib, args, rank, world, transport):
     """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3-5.
     transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads).
@@ -354,6 +459,13 @@ def ring_leg(lib, args, rank, world, transport):
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
                     "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
                     "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight)})
+        if os.environ.get("PG_BENCH_ONE_GPU") == "1":
+            res["rccl_native"] = "skipped: ranks share one GPU (RCCL refuses duplicate devices)"
+        else:
+            try:
+                res["rccl_native"] = native_crosscheck(lib, h, rank, world, x, dt)
+            except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
+                res["rccl_native"] = {"error": f"{type(e).__name__}: {e}"}
         # host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)
         xh = x.cpu().numpy()
         oh = np.empty(max(ln, 1), dtype=xh.dtype)
@@ -423,7 +535,8 @@ def main():
     wall, region_mean_ms, stamped_ms = kernel_leg(lib, args, rank, world)
     wall_max = max_over_ranks(wall, world)
     bytes_per_step = 3 * N_ELEMS * 8
-    mean_launch_ms = sum_over_ranks(region_mean_ms, world) / world
+    per_rank_ms = gather_over_ranks(region_mean_ms, rank, world)
+    mean_launch_ms = sum(per_rank_ms) / world
     achieved_gbs = bytes_per_step / (mean_launch_ms * 1e-3) / 1e9
     value = world * bytes_per_step * args.steps / wall_max / GIB
 
@@ -464,7 +577,11 @@ def main():
                                    "(includes the ~1 us kernel boundaries)",
                          "kernel_stamped_mean_ms": round(float(np.mean(stamped_ms)), 5),
                          "kernel_stamped_min_ms": round(float(np.min(stamped_ms)), 5),
-                         "bytes_per_launch": bytes_per_step},
+                         "bytes_per_launch": bytes_per_step,
+                         "per_gpu_gbs": None if world == 1 else {
+                             "min": round(bytes_per_step / max(per_rank_ms) / 1e6, 1),
+                             "median": round(bytes_per_step / float(np.median(per_rank_ms)) / 1e6, 1),
+                             "max": round(bytes_per_step / min(per_rank_ms) / 1e6, 1)}},
             "cpu_baseline": cpu,
             "host_staged": host,
             "config1": cfg1,
