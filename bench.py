@@ -250,7 +250,7 @@ def host_leg(lib, reps=3):
                      "pcie_gbs": round(3 * n * 8 / dt_ / 1e9, 2)}
         del d, s_
     out["note"] = ("256 MiB double sum, dst/src in host memory: threaded H2D dst+src, reduce, threaded "
-                   "D2H dst (PG_COPY_THREADS, default 4); pcie_gbs counts the 3*n*8 bytes that cross PCIe")
+                   "D2H dst (PG_COPY_THREADS, default 1); pcie_gbs counts the 3*n*8 bytes that cross PCIe")
     return out
 
 

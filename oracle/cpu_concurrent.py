@@ -46,7 +46,11 @@ def main():
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--seconds", type=float, default=5.0)
     a = ap.parse_args()
-    cores = sorted(os.sched_getaffinity(0))[: a.procs]
+    # spread over the allowed cores: adjacent cores share a CCD (and its link to
+    # the memory controllers) on EPYC, which would measure one CCD, not W ranks
+    allowed = sorted(os.sched_getaffinity(0))
+    k = min(a.procs, len(allowed))
+    cores = [allowed[(i * len(allowed)) // k] for i in range(k)]
     ctx = mp.get_context("fork")            # this process never touched a GPU
     start, q = ctx.Event(), ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(c, a.seconds, start, q)) for c in cores]
