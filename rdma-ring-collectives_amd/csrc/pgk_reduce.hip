@@ -247,13 +247,19 @@ int cu_count() {
   return g_cu_count[dev];
 }
 
-unsigned grid_for(size_t work_items_per_block_units) {
-  size_t g = work_items_per_block_units ? work_items_per_block_units : 1;
+// The AQL dispatch packet holds the grid size in WORK-ITEMS as 32 bits, so
+// gridDim.x * blockDim.x must stay below 2^32; the kernels grid-stride over
+// whatever a capped grid does not cover (> 64 GiB per operand on the vector
+// path, > 4 Gi elements on the scalar one).
+unsigned grid_cap(unsigned block) { return (unsigned)(0xFFFFFFFFull / block); }
+
+unsigned grid_for(size_t blocks, unsigned block) {
+  size_t g = blocks ? blocks : 1;
   if (g_blocks_per_cu > 0) {
     size_t cap = (size_t)cu_count() * (size_t)g_blocks_per_cu;
     if (g > cap) g = cap;
   }
-  if (g > 0x7fffffffu) g = 0x7fffffffu;
+  if (g > grid_cap(block)) g = grid_cap(block);
   return (unsigned)g;
 }
 
@@ -278,10 +284,10 @@ Plan plan_for(const void* out, const void* a, const void* b, size_t n, size_t es
     p.tail = (unsigned)(rest % W);
     size_t tile = (size_t)g_block * (size_t)g_unroll;
     size_t tiles = (p.nvec + tile - 1) / tile;
-    p.grid = grid_for(tiles);
+    p.grid = grid_for(tiles, (unsigned)g_block);
   } else {
     p.vec = false;
-    p.grid = grid_for((n + kScalarBlock - 1) / kScalarBlock);
+    p.grid = grid_for((n + kScalarBlock - 1) / kScalarBlock, kScalarBlock);
   }
   return p;
 }
@@ -363,7 +369,7 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
     size_t nvec = (n - head) / W, tail = (n - head) % W;
     size_t g = (nvec + kMultiBlock - 1) / kMultiBlock;
     if (g == 0) g = 1;
-    if (g > 0x7fffffff) g = 0x7fffffff;
+    if (g > grid_cap(kMultiBlock)) g = grid_cap(kMultiBlock);
     dim3 grid((unsigned)g), block(kMultiBlock);
     switch (nsrc) {
 #define PGK_MULTI_CASE(K) \

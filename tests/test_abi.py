@@ -68,6 +68,10 @@ def test_launch_geometry(lib):
     assert lib.pgk_launch_geometry(1 << 25, 1, ctypes.byref(g), ctypes.byref(b)) == 0
     assert b.value in (256, 512, 1024) and 1 <= g.value
     assert lib.pgk_launch_geometry(16, 7, None, None) == -1
+    # the dispatch packet's grid size is 32-bit in work-items: any n stays below 2^32
+    for n, dt in ((1 << 40, 1), (1 << 36, 0), ((1 << 31) - 1, 1), (1 << 33, 0)):
+        assert lib.pgk_launch_geometry(n, dt, ctypes.byref(g), ctypes.byref(b)) == 0
+        assert 1 <= g.value and g.value * b.value < 1 << 32, (n, dt, g.value, b.value)
 
 
 def test_connect_without_gpu_fails_cleanly(lib):

@@ -11,6 +11,7 @@ import hashlib
 import numpy as np
 import pytest
 
+import pgamd
 from gpu_util import ptr, same_bits_nan_aware, stream, to_dev, to_host
 
 pytestmark = pytest.mark.gpu
@@ -137,6 +138,34 @@ def test_full_size_config2(gpu, lib, oracle):
         assert got.tobytes() == oracle.reduce(a, b, dt, op).tobytes()
         del got
         torch.cuda.empty_cache()
+
+
+def test_maximum_counts(gpu, lib):
+    """The API's largest count (INT_MAX elements, include/pg.h `int count`) on the
+    vector path and on the element-wise path (dst one element off src's 16-B
+    phase), then an element-wise launch over 2^32 + 3 int32 (16 GiB operands)
+    whose grid is capped at 2^32 work-items and grid-strides over the rest:
+    every element is reduced exactly once, nothing past n is touched."""
+    torch = gpu
+    n = (1 << 31) - 1
+    d = torch.full((n + 2,), 1, dtype=torch.int32, device="cuda")
+    s = torch.full((n + 2,), 2, dtype=torch.int32, device="cuda")
+    assert lib.pgk_reduce(d.data_ptr(), s.data_ptr(), n, 0, 0, None) == 0, pgamd.last_error()
+    torch.cuda.synchronize()
+    assert bool(d[:n].eq(3).all()) and d[n:].tolist() == [1, 1]
+    assert lib.pgk_reduce(d.data_ptr() + 4, s.data_ptr(), n, 0, 0, None) == 0, pgamd.last_error()
+    torch.cuda.synchronize()
+    assert int(d[0]) == 3 and bool(d[1:n].eq(5).all()) and d[n:].tolist() == [3, 1]
+    del d, s
+    torch.cuda.empty_cache()
+    n = (1 << 32) + 3
+    d = torch.full((n + 2,), 1, dtype=torch.int32, device="cuda")
+    s = torch.full((n + 2,), 2, dtype=torch.int32, device="cuda")
+    assert lib.pgk_reduce(d.data_ptr() + 4, s.data_ptr(), n, 0, 0, None) == 0, pgamd.last_error()
+    torch.cuda.synchronize()
+    assert int(d[0]) == 1 and bool(d[1:n + 1].eq(3).all()) and int(d[n + 1]) == 1
+    del d, s
+    torch.cuda.empty_cache()
 
 
 def test_invalid_arguments(gpu, lib):
