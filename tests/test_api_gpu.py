@@ -314,3 +314,27 @@ def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch):
                             count, dt, op, 0, 4096, 4, True))
         for a, b in zip(*outs):
             assert a.tobytes() == b.tobytes(), (dt, op)
+
+
+@pytest.mark.parametrize("world,count,eager", [(4, 100, 4096), (8, 3, 4096), (3, 1000, 0), (5, 4099, 0)])
+def test_all_gather_in_place(gpu, lib, oracle, world, count, eager):
+    """pg_all_gather(NULL, recvbuf, ...): each rank's contribution already sits
+    in its own slot of recvbuf (reference src/pg.c:295,302); the other slots hold
+    garbage that must be overwritten.  Eager one-shot and ring."""
+    torch = gpu
+    for dt in (0, 1):
+        xs = [oracle.fill(count, dt, 0, 7000 + r) for r in range(world)]
+        want = oracle.ring_all_gather(xs, dt)
+        for on_dev in (True, False):
+            recvs = []
+            for r in range(world):
+                buf = np.full(count * world, -7, NP[dt])
+                buf[r * count:(r + 1) * count] = xs[r]
+                recvs.append(buf)
+            R = [to_dev(torch, b) for b in recvs] if on_dev else recvs
+            rp = (ctypes.c_void_p * world)(*[(ptr(b) if on_dev else b.ctypes.data) for b in R])
+            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_GATHER, None, rp, count, dt, 0, 0, eager, 4) == 0, \
+                pgamd.last_error()
+            for r in range(world):
+                got = to_host(torch, R[r]) if on_dev else R[r]
+                assert got.tobytes() == want[r].tobytes(), (world, count, eager, dt, on_dev, r)
