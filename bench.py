@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
     ap.add_argument("--transports", default="xgmi,rccl", help="ring-leg transports, comma separated")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
+    ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
 
 
@@ -85,6 +86,15 @@ def dist_setup(args):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
     return rank, world, local
+
+
+_T0 = time.perf_counter()
+
+
+def progress(rank, msg):
+    """One line per leg on stderr (rank-tagged, seconds since start): the
+    driver and gpurun read a silent run as hung, and a stalled leg is named."""
+    print(f"[bench r{rank} +{time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def barrier(world):
@@ -172,6 +182,59 @@ def kernel_leg(lib, args, rank, world):
     del dst, src
     torch.cuda.empty_cache()
     return t1 - t0, region_mean_ms, stamped
+
+
+SWEEP_BYTES = (64 << 20, 128 << 20, 256 << 20, 512 << 20, 1 << 30)   # per operand, north_star: >= 64 MiB
+SWEEP_POOL = 4 << 30
+
+
+def size_leg(lib, rank, world, reps=20):
+    """The kernel on power-of-two chunks of 64 MiB .. 1 GiB per operand, int32
+    and double sum (the metric's two cases), plus int32/double prod at 256 MiB.
+
+    One 4 GiB pool is carved into dst/src pairs of the size under test and the
+    launches rotate over all of them, so every launch streams from HBM (the
+    pool is 16x the 256 MiB Infinity Cache).  Each row is timed like the
+    primary measurement (HIP events bracketing `reps` launches on the launch
+    stream) with every rank launching at once after a barrier; the row keeps
+    the slowest rank's time."""
+    pool = torch.empty(SWEEP_POOL // 8, dtype=torch.float64, device="cuda")
+    pool.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(99 + rank))
+    base = pool.data_ptr()
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cases = [(pgamd.DT_DOUBLE, pgamd.OP_SUM, SWEEP_BYTES), (pgamd.DT_INT32, pgamd.OP_SUM, SWEEP_BYTES),
+             (pgamd.DT_DOUBLE, pgamd.OP_PROD, (256 << 20,)), (pgamd.DT_INT32, pgamd.OP_PROD, (256 << 20,))]
+    rows = []
+    for dt, op, sizes in cases:
+        for size in sizes:
+            n = size // pgamd.ELEM_SIZE[dt]
+            pairs = SWEEP_POOL // (2 * size)
+
+            def launch(i):
+                d = base + 2 * size * (i % pairs)
+                if lib.pgk_reduce(d, d + size, n, dt, op, sh) != 0:
+                    raise RuntimeError(pgamd.last_error())
+
+            for i in range(4):
+                launch(i)
+            torch.cuda.synchronize()
+            barrier(world)
+            e0.record(stream)
+            for i in range(reps):
+                launch(i)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+            gbs = 3 * size / (ms * 1e-3) / 1e9
+            rows.append(["f64" if dt == pgamd.DT_DOUBLE else "i32", "sum" if op == pgamd.OP_SUM else "prod",
+                         size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4)])
+    del pool
+    torch.cuda.empty_cache()
+    return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac"], "rows": rows,
+            "timing": f"HIP events bracketing {reps} launches rotating over a 4 GiB pool, all ranks at once; "
+                      "slowest rank; GB/s counts 3 x bytes_per_operand (read dst, read src, write dst)"}
 
 
 def cpu_baseline(args):
@@ -323,25 +386,29 @@ def _timed_rs(lib, h, x, out, count, dt, op, reps, world):
     return max_over_ranks(time.perf_counter() - t0, world) / reps
 
 
-def _pattern(count, rank, world, dt, op):
+def _pattern(count, rank, world, dt, op, off=0, ln=None):
     """Inputs whose W-rank reduction is exact in both dtypes, so every rank can
     check its block on the device: sum -> (i % 1000) + rank; prod -> powers of
-    two (double) / {1, 2, -1} (int32)."""
+    two (double) / {1, 2, -1} (int32).  Elements [off, off + ln) of rank
+    `rank`'s input (default: all `count`), built in the target dtype without
+    full-size int64 temporaries."""
     tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
-    i = torch.arange(count, device="cuda", dtype=torch.int64)
+    ln = count - off if ln is None else ln
+    i = torch.arange(off, off + ln, device="cuda", dtype=torch.int64)
     if op == pgamd.OP_SUM:
-        return ((i % 1000) + rank).to(tdt)
-    k = (i + rank) % 3
+        i.remainder_(1000).add_(rank)
+        return i.to(tdt)
+    i.add_(rank).remainder_(3)
     if dt == pgamd.DT_DOUBLE:
-        return torch.pow(2.0, (k - 1).to(torch.float64))
-    return torch.where(k == 2, -1, k + 1).to(torch.int32)
+        return torch.pow(2.0, (i - 1).to(torch.float64))
+    return torch.where(i == 2, -1, i + 1).to(torch.int32)
 
 
 def _expected_block(count, off, ln, world, dt, op):
     tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
     acc = None
     for q in range(world):
-        v = _pattern(count, q, world, dt, op)[off:off + ln].to(torch.float64 if dt == pgamd.DT_DOUBLE else torch.int64)
+        v = _pattern(count, q, world, dt, op, off, ln).to(torch.float64 if dt == pgamd.DT_DOUBLE else torch.int64)
         acc = v if acc is None else (acc + v if op == pgamd.OP_SUM else acc * v)
     if dt == pgamd.DT_INT32:
         acc = ((acc + 2**31) % 2**32 - 2**31)
@@ -439,6 +506,7 @@ def ring_leg(lib, args, rank, world, transport):
     os.environ["PG_TRANSPORT"] = transport
     os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + (17 if transport == "rccl" else 19))
     h = ctypes.c_void_p()
+    progress(rank, f"  {transport}: connect_process_group")
     if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
         raise RuntimeError("connect_process_group: " + pgamd.last_error())
     try:
@@ -449,9 +517,11 @@ def ring_leg(lib, args, rank, world, transport):
         off, ln = pgamd.block_range(count, world, rank)
         out = torch.empty(max(ln, 1), dtype=x.dtype, device="cuda")
         torch.cuda.synchronize()
+        progress(rank, f"  {transport}: correctness probe, {count} elements")
         pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h), "ring RS")
         ok = bool(torch.equal(out[:ln], _expected_block(count, off, ln, world, dt, pgamd.OP_SUM)))
         res["ok"] = sum_over_ranks(1.0 if ok else 0.0, world) == world
+        progress(rank, f"  {transport}: timed reduce-scatter")
         wall = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, args.ring_steps, world)
         payload = count * es                       # per rank
         res.update({"ms_per_reduce_scatter": round(wall * 1e3, 3),
@@ -462,11 +532,13 @@ def ring_leg(lib, args, rank, world, transport):
         if os.environ.get("PG_BENCH_ONE_GPU") == "1":
             res["rccl_native"] = "skipped: ranks share one GPU (RCCL refuses duplicate devices)"
         else:
+            progress(rank, f"  {transport}: RCCL-native cross-check")
             try:
                 res["rccl_native"] = native_crosscheck(lib, h, rank, world, x, dt)
             except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
                 res["rccl_native"] = {"error": f"{type(e).__name__}: {e}"}
         # host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)
+        progress(rank, f"  {transport}: host-buffer reduce-scatter")
         xh = x.cpu().numpy()
         oh = np.empty(max(ln, 1), dtype=xh.dtype)
         barrier(world)
@@ -480,6 +552,7 @@ def ring_leg(lib, args, rank, world, transport):
         del xh, oh
         rounds = world - 1
         if world == 4:                                    # config 3: PG_CHUNK_BYTES sweep
+            progress(rank, f"  {transport}: chunk sweep")
             rows = []
             for cb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20):
                 hd.chunk_bytes = cb
@@ -490,6 +563,7 @@ def ring_leg(lib, args, rank, world, transport):
             res["chunk_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes"],
                                   "rows": rows}
         if world == 8:                                    # config 4: PG_INFLIGHT sweep
+            progress(rank, f"  {transport}: inflight sweep")
             rows = []
             for inf in (1, 2, 4, 8, 16):
                 hd.inflight = inf
@@ -500,6 +574,7 @@ def ring_leg(lib, args, rank, world, transport):
         del x, out
         torch.cuda.empty_cache()
         if world == 8:                                    # config 5: prod, eager and 2 GiB mixed
+            progress(rank, f"  {transport}: config 5")
             cfg5 = []
             for dt5, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
                 small = 4096 // pgamd.ELEM_SIZE[dt5]
@@ -532,6 +607,7 @@ def main():
     args = parse()
     rank, world, local = dist_setup(args)
     lib = pgamd.load()
+    progress(rank, f"kernel leg (world {world}, device {local})")
     wall, region_mean_ms, stamped_ms = kernel_leg(lib, args, rank, world)
     wall_max = max_over_ranks(wall, world)
     bytes_per_step = 3 * N_ELEMS * 8
@@ -540,11 +616,21 @@ def main():
     achieved_gbs = bytes_per_step / (mean_launch_ms * 1e-3) / 1e9
     value = world * bytes_per_step * args.steps / wall_max / GIB
 
+    sizes = None
+    if not args.no_sizes:
+        progress(rank, "kernel size table")
+        try:
+            sizes = size_leg(lib, rank, world)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the primary line
+            sizes = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     host = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        progress(rank, "cpu baseline")
         cpu = cpu_baseline(args)
     if world == 1 and not args.no_host:
+        progress(rank, "host-memory leg")
         try:
             host = host_leg(lib)
         except Exception as e:
@@ -582,6 +668,7 @@ def main():
                              "min": round(bytes_per_step / max(per_rank_ms) / 1e6, 1),
                              "median": round(bytes_per_step / float(np.median(per_rank_ms)) / 1e6, 1),
                              "max": round(bytes_per_step / min(per_rank_ms) / 1e6, 1)}},
+            "kernel_sizes": sizes,
             "cpu_baseline": cpu,
             "host_staged": host,
             "config1": cfg1,
@@ -608,6 +695,7 @@ def main():
         dog.daemon = True
         dog.start()
         for transport in args.transports.split(","):
+            progress(rank, f"ring leg: {transport}")
             try:
                 ring[transport] = ring_leg(lib, args, rank, world, transport)
             except Exception as e:  # the primary measurement stands on its own

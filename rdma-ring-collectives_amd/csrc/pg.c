@@ -37,6 +37,26 @@ void pg_set_error(const char *fmt, ...) {
 
 const char *pg_last_error(void) { return g_pg_err; }
 
+/* PG_TRACE=1: one stderr line per transport phase (rank, monotonic ms), to
+ * name the phase a stalled multi-process call is in. */
+void pg_trace(const struct pg *pg, const char *fmt, ...) {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("PG_TRACE");
+    on = e && *e == '1';
+  }
+  if (!on) return;
+  char msg[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  fprintf(stderr, "[pg r%d %ld.%03ld] %s\n", pg ? pg->rank : -1, (long)ts.tv_sec, ts.tv_nsec / 1000000L, msg);
+  fflush(stderr);
+}
+
 /* ---- small helpers ---------------------------------------------------------- */
 
 size_t pg_elem_size(int dt) {                 /* reference src/pg.c:109-115 */

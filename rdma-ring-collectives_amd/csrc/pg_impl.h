@@ -77,6 +77,7 @@ struct pg_impl {
 
 /* pg.c */
 void pg_set_error(const char *fmt, ...);
+void pg_trace(const struct pg *pg, const char *fmt, ...);
 int pg_ensure(void **buf, size_t *cap, size_t bytes);   /* hipMalloc-grow */
 int pg_stream_wait(hipStream_t s);                        /* bounded spin, then block */
 int pg_copy_parallel(void *dst, const void *src, size_t bytes);  /* host<->device, threaded */

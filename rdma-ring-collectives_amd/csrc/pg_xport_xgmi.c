@@ -11,13 +11,17 @@
  * which is bit-identical to the RCCL ring and to the oracle's ring simulator.
  * This is the "fused receive-reduce" + "multi-link" rows of SURVEY.md §8f.
  *
- * Memory: each rank owns one IPC-exportable HBM allocation split into
- * contribution slots X0/X1 and all-reduce result slots R0/R1 (double-buffered
- * by call parity), mapped into every peer with hipIpcOpenMemHandle.  A call
- * copies its input into X[parity], meets the others at a host barrier on the
- * bootstrap star (pg_boot.c), then reads.  Double buffering makes one barrier
- * per call enough: a slot is rewritten two calls later, and every rank passed
- * the intervening call's barrier only after finishing its reads.
+ * Memory: each rank owns up to two IPC-exportable HBM regions, each mapped
+ * into every peer with hipIpcOpenMemHandle and double-buffered by call parity:
+ * contribution slots X0/X1 (used only when an input cannot be read in place)
+ * and all-reduce result slots R0/R1 (used only by the reduce-scatter + gather
+ * form of the all-reduce).  A region is allocated the first time a call needs
+ * it, so a zero-copy reduce-scatter holds no exchange memory at all.  A call
+ * that uses X copies its input into X[parity], meets the others at a host
+ * barrier (node-local shared memory, pg_boot.c), then reads.  Double
+ * buffering makes one barrier per call enough: a slot is rewritten two calls
+ * later, and every rank passed the intervening call's barrier only after
+ * finishing its reads.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -27,7 +31,8 @@
 
 #include "pg_impl.h"
 
-#define XG_SLOTS 4              /* X0, X1, R0, R1 */
+#define XG_REG_X 0              /* contribution slots X0, X1 */
+#define XG_REG_R 1              /* all-reduce result slots R0, R1 */
 #define XG_IMPORTS 2            /* mapped input allocations cached per peer */
 
 struct xg_import {
@@ -37,10 +42,14 @@ struct xg_import {
 };
 #define XG_GRANULE (64ull << 20)
 
-struct xgmi_ctx {
-  void *mem;                    /* my allocation: XG_SLOTS * cap bytes      */
-  size_t cap;                   /* bytes per slot                           */
+struct xg_region {
+  void *mem;                    /* my allocation: 2 slots of cap bytes      */
+  size_t cap;                   /* bytes per slot (0: not allocated yet)    */
   void **peer;                  /* peer[q] = rank q's allocation, mapped    */
+};
+
+struct xgmi_ctx {
+  struct xg_region reg[2];      /* XG_REG_X, XG_REG_R                       */
   size_t oneshot_max;           /* all-reduce at most this many bytes: one-shot */
   void *bar;                    /* node-local shm barrier (pg_boot.c), or NULL */
   int zc;                       /* zero-copy inputs allowed (PG_XGMI_ZERO_COPY) */
@@ -55,6 +64,18 @@ struct xgmi_ctx {
 
 static void drop_imports(struct pg *pg, struct xgmi_ctx *x);
 
+/* ROCm 7.2: hipIpcOpenMemHandle never returns for an allocation whose size has
+ * bit 31 set (2 GiB, 2 GiB + 2 MiB, 3 GiB, 6 GiB stall; 2 GiB - 2 MiB, 4, 5,
+ * 8, 12 GiB open in < 1 ms; measured on MI355X, tools/ipc_probe3.py).  So no
+ * allocation of that size is ever exported: our own slot memory is padded to
+ * the next multiple of 4 GiB, and a caller's input living in such an
+ * allocation takes the slot copy instead of zero-copy. */
+static int ipc_size_ok(size_t bytes) { return (bytes & (1ull << 31)) == 0; }
+
+static size_t ipc_safe_size(size_t bytes) {
+  return ipc_size_ok(bytes) ? bytes : (bytes + (4ull << 30) - 1) & ~((4ull << 30) - 1);
+}
+
 static struct xgmi_ctx *ctx_of(struct pg *pg) {
   return (struct xgmi_ctx *)((struct pg_impl *)pg->impl)->xctx;
 }
@@ -65,8 +86,10 @@ static double us_now(void) {
   return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
 }
 
-static char *slot(struct xgmi_ctx *x, int q, int which) {
-  return (char *)x->peer[q] + (size_t)which * x->cap;
+/* Rank q's slot `parity` of region `reg` (NULL while the region is unallocated). */
+static char *slot(struct xgmi_ctx *x, int reg, int q, int parity) {
+  const struct xg_region *g = &x->reg[reg];
+  return g->peer[q] ? (char *)g->peer[q] + (size_t)parity * g->cap : NULL;
 }
 
 /* All ranks of this transport share one node: shm barrier, TCP as fallback. */
@@ -76,22 +99,23 @@ static int barrier(struct pg *pg) {
   return x->bar ? pg_shm_barrier(pg, x->bar) : pg_boot_barrier(pg, im->boot_fds);
 }
 
-static void unmap_peers(struct pg *pg, struct xgmi_ctx *x) {
-  if (!x->peer) return;
+static void unmap_peers(struct pg *pg, struct xg_region *g) {
+  if (!g->peer) return;
   for (int q = 0; q < pg->world_size; ++q)
-    if (q != pg->rank && x->peer[q]) hipIpcCloseMemHandle(x->peer[q]);
-  memset(x->peer, 0, sizeof(void *) * (size_t)pg->world_size);
+    if (q != pg->rank && g->peer[q]) hipIpcCloseMemHandle(g->peer[q]);
+  memset(g->peer, 0, sizeof(void *) * (size_t)pg->world_size);
 }
 
-static void unmap(struct pg *pg, struct xgmi_ctx *x) {
-  unmap_peers(pg, x);
-  if (x->mem) hipFree(x->mem);
-  x->mem = NULL;
-  x->cap = 0;
+static void unmap(struct pg *pg, struct xg_region *g) {
+  unmap_peers(pg, g);
+  if (g->mem) hipFree(g->mem);
+  g->mem = NULL;
+  g->cap = 0;
 }
 
-/* Collective: every rank calls with the same `bytes` (same count), so every
- * rank grows in the same call to the same size.
+/* Region `reg` holds slots of at least `bytes`.  Collective: every rank calls
+ * it at the same point of the same call with the same `bytes` (same count),
+ * so every rank grows in the same call to the same size.
  *
  * Growth order matters (observed on ROCm 7.2, tests/test_xgmi_gpu.py::
  * test_xgmi_slot_growth): unmapping the peers' old slots, then allocating and
@@ -99,15 +123,17 @@ static void unmap(struct pg *pg, struct xgmi_ctx *x) {
  * So the replacement is allocated and exported while every old import is
  * still mapped, and the old allocation is freed only after all ranks have
  * dropped their mappings of it. */
-static int ensure(struct pg *pg, size_t bytes) {
+static int ensure(struct pg *pg, int reg, size_t bytes) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
-  struct xgmi_ctx *x = ctx_of(pg);
-  if (bytes <= x->cap && x->mem) return 0;
-  size_t cap = x->cap ? x->cap : XG_GRANULE;
+  struct xg_region *g = &ctx_of(pg)->reg[reg];
+  if (bytes <= g->cap && g->mem) return 0;
+  size_t cap = g->cap ? g->cap : XG_GRANULE;
   while (cap < bytes) cap *= 2;
-  if (x->mem && barrier(pg)) return -1;      /* nobody still reads the old slots */
+  pg_trace(pg, "xgmi ensure: region %d grows %zu -> %zu bytes per slot", reg, g->cap, cap);
+  if (g->mem && barrier(pg)) return -1;      /* nobody still reads the old slots */
   void *fresh = NULL;
-  PG_CHECK_HIP(hipMalloc(&fresh, cap * XG_SLOTS));
+  PG_CHECK_HIP(hipMalloc(&fresh, ipc_safe_size(cap * 2)));
+  pg_trace(pg, "xgmi ensure: allocated");
   hipIpcMemHandle_t mine, *all = (hipIpcMemHandle_t *)malloc(sizeof(hipIpcMemHandle_t) * (size_t)pg->world_size);
   if (!all) { hipFree(fresh); pg_set_error("xgmi: out of host memory"); return -1; }
   hipError_t e = hipIpcGetMemHandle(&mine, fresh);
@@ -117,18 +143,22 @@ static int ensure(struct pg *pg, size_t bytes) {
     pg_set_error("xgmi: hipIpcGetMemHandle: %s", hipGetErrorString(e));
     return -1;
   }
-  if (x->mem) {
-    unmap_peers(pg, x);
+  pg_trace(pg, "xgmi ensure: exported");
+  if (g->mem) {
+    unmap_peers(pg, g);
+    pg_trace(pg, "xgmi ensure: old peer slots unmapped");
     if (barrier(pg)) { free(all); hipFree(fresh); return -1; }   /* nobody maps my old slots */
-    hipFree(x->mem);
+    hipFree(g->mem);
+    pg_trace(pg, "xgmi ensure: old slots freed");
   }
-  x->mem = fresh;
-  x->cap = cap;
-  x->peer[pg->rank] = x->mem;
+  g->mem = fresh;
+  g->cap = cap;
+  g->peer[pg->rank] = g->mem;
   if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) { free(all); return -1; }
   for (int q = 0; q < pg->world_size; ++q) {
     if (q == pg->rank) continue;
-    e = hipIpcOpenMemHandle(&x->peer[q], all[q], hipIpcMemLazyEnablePeerAccess);
+    e = hipIpcOpenMemHandle(&g->peer[q], all[q], hipIpcMemLazyEnablePeerAccess);
+    pg_trace(pg, "xgmi ensure: opened rank %d's slots: %s", q, hipGetErrorString(e));
     if (e != hipSuccess) {
       free(all);
       pg_set_error("xgmi: hipIpcOpenMemHandle(rank %d): %s", q, hipGetErrorString(e));
@@ -145,8 +175,10 @@ int pg_xport_xgmi_init(struct pg *pg) {
   struct xgmi_ctx *x = (struct xgmi_ctx *)calloc(1, sizeof(*x));
   if (!x) return -1;
   im->xctx = x;
-  x->peer = (void **)calloc((size_t)pg->world_size, sizeof(void *));
-  if (!x->peer) { pg_set_error("xgmi: out of host memory"); return -1; }
+  for (int g = 0; g < 2; ++g) {
+    x->reg[g].peer = (void **)calloc((size_t)pg->world_size, sizeof(void *));
+    if (!x->reg[g].peer) { pg_set_error("xgmi: out of host memory"); return -1; }
+  }
   x->oneshot_max = 1u << 20;
   const char *e = getenv("PG_ONESHOT_MAX");
   if (e && *e) x->oneshot_max = (size_t)strtoull(e, NULL, 0);
@@ -164,13 +196,16 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
   if (!x) return;
-  /* peers may still be reading my last contribution: meet them first */
-  if (x->mem && im->boot_fds) barrier(pg);
+  /* peers may still be reading my last contribution: meet them first
+   * (regions are allocated collectively, so every rank takes this branch alike) */
+  if ((x->reg[XG_REG_X].mem || x->reg[XG_REG_R].mem) && im->boot_fds) barrier(pg);
   drop_imports(pg, x);
   free(x->imp);
-  unmap(pg, x);
+  for (int g = 0; g < 2; ++g) {
+    unmap(pg, &x->reg[g]);
+    free(x->reg[g].peer);
+  }
   pg_shm_close(x->bar);
-  free(x->peer);
   free(x);
   im->xctx = NULL;
 }
@@ -217,6 +252,7 @@ static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
     (void)hipGetLastError();
     return 0;
   }
+  if (!ipc_size_ok(size)) return 0;           /* peers could not open it: slot copy */
   if (!x->exp_valid || x->exp_bid != bid || x->exp_base != base) {
     x->exp_valid = 0;
     if (hipIpcGetMemHandle(&x->exp_h, base) != hipSuccess) { (void)hipGetLastError(); return 0; }
@@ -275,6 +311,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   if (x->zc && x->bar && bytes) {
     struct xg_desc mine;
     if (!in_dev || may_alias_out || !export_input(x, in, &mine)) memset(&mine, 0, sizeof(mine));
+    pg_trace(pg, "xgmi share: input %p exported=%d", in, mine.ok);
     descs(x)[r] = mine;
     if (barrier(pg)) return -1;
     struct xg_desc all[16];
@@ -285,6 +322,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
     if (all_ok) {
       for (int q = 0; q < W; ++q) {
         by_rank[q] = q == r ? (const char *)in : import_input(x, q, &all[q]);
+        pg_trace(pg, "xgmi share: rank %d's input at %p", q, (const void *)by_rank[q]);
         if (!by_rank[q]) {
           pg_set_error("xgmi: could not map rank %d's input", q);
           *fail = 1;
@@ -295,7 +333,9 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
     }
     /* somebody's input cannot be shared in place: everybody copies */
   }
-  char *xs = slot(x, r, which);
+  /* every rank reaches this point in this call (the choice above is collective) */
+  if (bytes && ensure(pg, XG_REG_X, bytes)) return -1;
+  char *xs = slot(x, XG_REG_X, r, which);
   double t2 = us_now();
   if (bytes) {
     if (in_dev && ((uintptr_t)in & 3) == 0 && (bytes & 3) == 0) {
@@ -316,7 +356,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   int rc = barrier(pg);
   im->stats.copy_us += t3 - t2;
   im->stats.barrier_us += us_now() - t3;
-  for (int q = 0; q < W; ++q) by_rank[q] = slot(x, q, which);
+  for (int q = 0; q < W; ++q) by_rank[q] = slot(x, XG_REG_X, q, which);
   return rc;
 }
 
@@ -344,11 +384,13 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
   const void *srcs[16];
   for (int j = 0; j < W; ++j) srcs[j] = by_rank[(r + 1 + j) % W] + off_elems * es;
   double tk = us_now();
+  pg_trace(pg, "xgmi fold: %zu elements from %d ranks", len, W);
   if (pgk_reduce_multi(out, srcs, W, len, dt, op, (void *)im->red)) {
     pg_set_error("xgmi: %s", pgk_last_error());
     return -1;
   }
   if (pg_stream_wait(im->red)) return -1;
+  pg_trace(pg, "xgmi fold: done");
   im->stats.kernel_us += us_now() - tk;
   im->stats.reduce_launches += 1;
   im->stats.reduce_elems += (int64_t)len * (W - 1);
@@ -365,7 +407,6 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
-  if (ensure(pg, bytes)) return -1;
   int rd = is_dev(recvbuf), zc, fail;
   const char *by_rank[16];
   if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, len * es), by_rank,
@@ -412,7 +453,6 @@ static int gather(struct pg *pg, char *full, const char *const *by_rank, int cou
 int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t es = pg_elem_size(dt), slot_bytes = (size_t)count * es, total = slot_bytes * (size_t)pg->world_size;
-  if (ensure(pg, slot_bytes)) return -1;
   int rd = is_dev(recvbuf), zc, fail;
   const void *mine = sendbuf ? sendbuf : (const char *)recvbuf + (size_t)pg->rank * slot_bytes;
   const char *by_rank[16];
@@ -436,7 +476,6 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
-  if (ensure(pg, bytes)) return -1;
   int rd = is_dev(recvbuf), which = (int)(x->gen & 1), zc, fail;
   const char *by_rank[16];
   if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, bytes), by_rank, &zc,
@@ -464,12 +503,13 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     }
   } else {
     /* my block of the result goes to R[which] so that every rank can gather it */
-    if (!fail && fold_block(pg, slot(x, pg->rank, 2 + which) + off * es, by_rank, off, len, dt, op)) fail = 1;
+    if (ensure(pg, XG_REG_R, bytes)) return -1;
+    if (!fail && fold_block(pg, slot(x, XG_REG_R, pg->rank, which) + off * es, by_rank, off, len, dt, op)) fail = 1;
     double tb = us_now();
     if (barrier(pg)) return -1;
     im->stats.barrier_us += us_now() - tb;
     const char *res_by_rank[16];
-    for (int q = 0; q < pg->world_size; ++q) res_by_rank[q] = slot(x, q, 2 + which);
+    for (int q = 0; q < pg->world_size; ++q) res_by_rank[q] = slot(x, XG_REG_R, q, which);
     if (!fail && gather(pg, full, res_by_rank, count, 0, dt)) fail = 1;
   }
   if (finish(pg, zc, fail)) return -1;

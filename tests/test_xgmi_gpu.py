@@ -186,3 +186,71 @@ def test_xgmi_slot_growth(gpu, world):
                 p.kill()
     for rank, fails in results:
         assert not fails, (rank, fails)
+
+
+def _bit31_worker(rank, world, port, q):
+    """Allocations whose size has bit 31 set stall hipIpcOpenMemHandle on
+    ROCm 7.2 (tools/ipc_probe3.py).  600 MiB calls need 1 GiB slots, i.e. a
+    2 GiB two-slot region that the transport must pad: (a) a fresh input is
+    read in place and the all-reduce grows the result region; (b) an input
+    that lives in a 2 GiB allocation cannot be shared in place, so every rank
+    falls back to the slot copy together and grows the contribution region."""
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="60000")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        big = torch.empty(2 << 30, dtype=torch.uint8, device="cuda")          # exactly 2 GiB
+        for label, count in (("fresh input", (600 << 20) // 8), ("input in 2 GiB", (600 << 20) // 8)):
+            i = torch.arange(count, device="cuda", dtype=torch.int64)
+            if label == "input in 2 GiB":
+                x = big[:count * 8].view(torch.float64)
+                x.copy_(((i % 1000) + rank).to(torch.float64))
+            else:
+                x = ((i % 1000) + rank).to(torch.float64)
+            want = ((i % 1000) * world + world * (world - 1) // 2).to(torch.float64)
+            off, ln = pgamd.block_range(count, world, rank)
+            z = torch.empty(max(ln, 1), dtype=torch.float64, device="cuda")
+            if lib.pg_reduce_scatter(x.data_ptr(), z.data_ptr(), count, 1, 0, h) != 0 or \
+                    not torch.equal(z[:ln], want[off:off + ln]):
+                fails.append((label, "rs", pgamd.last_error()))
+            y = torch.empty(count, dtype=torch.float64, device="cuda")
+            if lib.pg_all_reduce(x.data_ptr(), y.data_ptr(), count, 1, 0, h) != 0 or not torch.equal(y, want):
+                fails.append((label, "ar", pgamd.last_error()))
+            del i, x, y, z, want
+            torch.cuda.empty_cache()
+        lib.pg_close(h)
+    except Exception as e:
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+def test_xgmi_ipc_bit31_sizes(gpu):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bit31_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=150))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)

@@ -8,7 +8,7 @@ tag=${1:-r01}
 export TMPDIR=/tmp
 tools/gpu_step.sh pytest_gpu 900 python -m pytest tests -m gpu -q
 tools/gpu_step.sh bench 400 python bench.py
-tools/profile_bench.sh "$tag" --steps 50 --warmup 10 --no-host
+tools/profile_bench.sh "$tag" --steps 50 --warmup 10 --no-host --no-sizes
 tools/gpu_step.sh sweep 600 python tools/sweep_kernel.py --quick
 tools/gpu_step.sh latency 300 python tools/latency.py --world 2
 PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
