@@ -204,6 +204,9 @@ def size_leg(lib, rank, world, reps=20):
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    stamp = (ctypes.c_void_p(), ctypes.c_void_p())
+    pgamd.check(lib.pgk_event_create(ctypes.byref(stamp[0])), "event")
+    pgamd.check(lib.pgk_event_create(ctypes.byref(stamp[1])), "event")
     cases = [(pgamd.DT_DOUBLE, pgamd.OP_SUM, SWEEP_BYTES), (pgamd.DT_INT32, pgamd.OP_SUM, SWEEP_BYTES),
              (pgamd.DT_DOUBLE, pgamd.OP_PROD, (256 << 20,)), (pgamd.DT_INT32, pgamd.OP_PROD, (256 << 20,))]
     rows = []
@@ -212,9 +215,11 @@ def size_leg(lib, rank, world, reps=20):
             n = size // pgamd.ELEM_SIZE[dt]
             pairs = SWEEP_POOL // (2 * size)
 
-            def launch(i):
+            def launch(i, ev=None):
                 d = base + 2 * size * (i % pairs)
-                if lib.pgk_reduce(d, d + size, n, dt, op, sh) != 0:
+                rc = (lib.pgk_reduce_timed(d, d + size, n, dt, op, sh, ev[0], ev[1]) if ev
+                      else lib.pgk_reduce(d, d + size, n, dt, op, sh))
+                if rc != 0:
                     raise RuntimeError(pgamd.last_error())
 
             for i in range(4):
@@ -228,13 +233,30 @@ def size_leg(lib, rank, world, reps=20):
             torch.cuda.synchronize()
             ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
             gbs = 3 * size / (ms * 1e-3) / 1e9
+            # kernel-stamped launches (the kernel alone, as rocprofv3 reports it)
+            st = []
+            for i in range(8):
+                launch(i, stamp)
+                torch.cuda.synchronize()
+                v = ctypes.c_float()
+                pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
+                st.append(v.value)
+            sms = max_over_ranks(float(np.median(st)), world)
+            sgbs = 3 * size / (sms * 1e-3) / 1e9
             rows.append(["f64" if dt == pgamd.DT_DOUBLE else "i32", "sum" if op == pgamd.OP_SUM else "prod",
-                         size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4)])
+                         size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4),
+                         round(sms * 1e3, 2), round(sgbs / HBM_PEAK_GBS, 4)])
+    lib.pgk_event_destroy(stamp[0])
+    lib.pgk_event_destroy(stamp[1])
     del pool
     torch.cuda.empty_cache()
-    return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac"], "rows": rows,
-            "timing": f"HIP events bracketing {reps} launches rotating over a 4 GiB pool, all ranks at once; "
-                      "slowest rank; GB/s counts 3 x bytes_per_operand (read dst, read src, write dst)"}
+    return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
+                        "stamped_frac"], "rows": rows,
+            "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
+                      "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
+                      "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
+                      "times it), slowest rank; GB/s and frac count 3 x bytes_per_operand (read dst, read src, "
+                      "write dst) against 8000 GB/s"}
 
 
 def cpu_baseline(args):

@@ -77,7 +77,8 @@ PG_API int pgk_synchronize(void);
 PG_API int pgk_tune(int blocks_per_cu, int nontemporal);
 
 /* Vector-kernel shape: threads per block x 16-byte vectors per operand each
- * thread keeps in flight.  Instantiated: 256x2, 256x4, 256x8, 512x2, 1024x1. */
+ * thread keeps in flight.  Instantiated: 256x2, 256x4, 256x8, 512x2, 1024x1;
+ * 0x0 (the default) picks by operand size (512x2 below 128 MiB, else 1024x1). */
 PG_API int pgk_tune_shape(int block, int unroll);
 
 /* pgk_reduce, with the kernel's own begin/end timestamps recorded into two

@@ -229,8 +229,19 @@ void set_err(const char* fmt, ...) {
 // Tuning (process-wide).  Measured on MI355X: see DESIGN.md "Kernel tuning".
 int g_blocks_per_cu = 0;   // one-shot grid: 6403 vs 6200 GB/s capped at 8/CU (sweep r01)
 int g_nontemporal = 1;
-int g_block = 1024;   // 1024x1: 6619 GB/s vs 6511 (256x4) at 256 MiB, sweep r01b
-int g_unroll = 1;
+// Vector shape: 0x0 = by size (shape_for); else forced by pgk_tune_shape.
+int g_block = 0;
+int g_unroll = 0;
+
+// Measured on MI355X (profiles/r01_sweep_kernel_shapes.csv, kernel-stamped,
+// f64 sum, nt): 512x2 leads below 128 MiB per operand (64 MiB: 31.1 us vs
+// 31.8 us for 1024x1), 1024x1 from 256 MiB up (256 MiB: 121.7 us vs 124.5 us
+// for 512x2; 1 GiB: 495 us vs 515 us).
+void shape_for(size_t bytes_per_operand, int* block, int* unroll) {
+  if (g_block) { *block = g_block; *unroll = g_unroll; return; }
+  if (bytes_per_operand < (128u << 20)) { *block = 512; *unroll = 2; }
+  else { *block = 1024; *unroll = 1; }
+}
 
 constexpr int kMaxDevices = 64;
 int g_cu_count[kMaxDevices];  // 0 = not queried yet
@@ -268,6 +279,7 @@ struct Plan {
   unsigned head, tail;
   size_t nvec;
   unsigned grid;
+  int block, unroll;   // vector path shape
 };
 
 Plan plan_for(const void* out, const void* a, const void* b, size_t n, size_t es) {
@@ -282,9 +294,10 @@ Plan plan_for(const void* out, const void* a, const void* b, size_t n, size_t es
     p.head = (unsigned)head;
     p.nvec = rest / W;
     p.tail = (unsigned)(rest % W);
-    size_t tile = (size_t)g_block * (size_t)g_unroll;
+    shape_for(n * es, &p.block, &p.unroll);
+    size_t tile = (size_t)p.block * (size_t)p.unroll;
     size_t tiles = (p.nvec + tile - 1) / tile;
-    p.grid = grid_for(tiles, (unsigned)g_block);
+    p.grid = grid_for(tiles, (unsigned)p.block);
   } else {
     p.vec = false;
     p.grid = grid_for((n + kScalarBlock - 1) / kScalarBlock, kScalarBlock);
@@ -306,7 +319,7 @@ void launch_shape(const Plan& p, T* out, const T* a, const T* b, hipStream_t s, 
 
 template <typename T, int OP, bool NT>
 void launch_vec(const Plan& p, T* out, const T* a, const T* b, hipStream_t s, Timing tm) {
-  switch (g_block * 16 + g_unroll) {
+  switch (p.block * 16 + p.unroll) {
     case 256 * 16 + 2: launch_shape<T, OP, NT, 256, 2>(p, out, a, b, s, tm); break;
     case 256 * 16 + 8: launch_shape<T, OP, NT, 256, 8>(p, out, a, b, s, tm); break;
     case 512 * 16 + 2: launch_shape<T, OP, NT, 512, 2>(p, out, a, b, s, tm); break;
@@ -518,7 +531,8 @@ int pgk_tune(int blocks_per_cu, int nontemporal) {
 }
 
 int pgk_tune_shape(int block, int unroll) {
-  const int ok = (block == 256 && (unroll == 2 || unroll == 4 || unroll == 8)) ||
+  const int ok = (block == 0 && unroll == 0) ||
+                 (block == 256 && (unroll == 2 || unroll == 4 || unroll == 8)) ||
                  (block == 512 && unroll == 2) || (block == 1024 && unroll == 1);
   if (!ok) { set_err("pgk: shape %dx%d not instantiated", block, unroll); return -1; }
   g_block = block;
@@ -553,7 +567,7 @@ int pgk_launch_geometry(size_t n, int dt, unsigned* grid, unsigned* block) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   Plan p = plan_for(nullptr, nullptr, nullptr, n, dt == PGK_DT_INT32 ? 4 : 8);
   if (grid) *grid = p.grid;
-  if (block) *block = p.vec ? (unsigned)g_block : (unsigned)kScalarBlock;
+  if (block) *block = p.vec ? (unsigned)p.block : (unsigned)kScalarBlock;
   return 0;
 }
 

@@ -110,7 +110,7 @@ def main():
             print(f"size={size:>11} {best[5]} {best[6]}: best {best[4]:8.1f} GB/s "
                   f"(bpc={best[7]} nt={best[8]} shape={best[9]}, {best[3]} us)", flush=True)
     lib.pgk_tune(0, 1)
-    lib.pgk_tune_shape(1024, 1)
+    lib.pgk_tune_shape(0, 0)
 
 
 if __name__ == "__main__":
