@@ -316,7 +316,8 @@ def cpu_baseline(args):
 
 def host_leg(lib, reps=3):
     """PCIe-inclusive rate of the same chunk reduce with dst/src in host memory
-    (pgx_reduce_host: threaded H2D of both operands, reduce, threaded D2H).
+    (pgx_reduce_host: 16 MiB pieces, uploads + reduce on the calling thread,
+    downloads on a helper thread, so both PCIe directions work at once).
     Reported, never `value`."""
     out = {}
     n = N_ELEMS
@@ -334,8 +335,9 @@ def host_leg(lib, reps=3):
                      "payload_gibs": round(n * 8 / dt_ / GIB, 2),
                      "pcie_gbs": round(3 * n * 8 / dt_ / 1e9, 2)}
         del d, s_
-    out["note"] = ("256 MiB double sum, dst/src in host memory: threaded H2D dst+src, reduce, threaded "
-                   "D2H dst (PG_COPY_THREADS, default 1); pcie_gbs counts the 3*n*8 bytes that cross PCIe")
+    out["note"] = ("256 MiB double sum, dst/src in host memory: 16 MiB pieces through 3 HBM slots, H2D dst+src "
+                   "and the reduce on one thread, D2H dst on another (both PCIe directions at once); pcie_gbs "
+                   "counts the 3*n*8 bytes that cross PCIe")
     return out
 
 

@@ -179,9 +179,11 @@ def test_invalid_arguments(gpu, lib):
 
 def test_reduce_host_staged(gpu, lib, oracle):
     """pgx_reduce_host: both operands in host memory (pageable and pinned),
-    chunked through HBM; identical to the oracle."""
+    piped through HBM slots (1 piece .. 25 pieces over 3 slots, ragged last
+    piece, default 32 MiB pieces); identical to the oracle."""
     torch = gpu
-    for dt, op, n, chunk in ((1, 0, (3 << 20) + 5, 1 << 20), (0, 1, 1000, 1 << 20), (1, 1, 1 << 22, 4 << 20)):
+    for dt, op, n, chunk in ((1, 0, (3 << 20) + 5, 1 << 20), (0, 1, 1000, 1 << 20), (1, 1, 1 << 22, 4 << 20),
+                             (0, 0, (5 << 20) + 7, 1 << 20), (1, 0, (1 << 23) + 1, 0)):
         a, b = oracle.fill(n, dt, op, 51), oracle.fill(n, dt, op, 52)
         want = oracle.reduce(a, b, dt, op)
         d = a.copy()
