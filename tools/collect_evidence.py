@@ -33,8 +33,13 @@ def main():
                      ("pytest_gpu.log", f"{tag}_pytest_gpu.log")):
         if (OUT / src).exists():
             shutil.copy(OUT / src, PROF / dst)
-    if (OUT / "bench_n2.log").exists():
-        (PROF / f"{tag}_bench_n2_onegpu_rehearsal.json").write_text(json.dumps(first_json(OUT / "bench_n2.log")) + "\n")
+    for w in (2, 4, 8):
+        if (OUT / f"bench_n{w}.log").exists():
+            (PROF / f"{tag}_bench_n{w}_onegpu_rehearsal.json").write_text(
+                json.dumps(first_json(OUT / f"bench_n{w}.log")) + "\n")
+    if (OUT / "host_pipe.log").exists():
+        (PROF / f"{tag}_host_pipe_probe.txt").write_text(
+            "".join(l + "\n" for l in (OUT / "host_pipe.log").read_text().splitlines() if "amdgpu.ids" not in l))
     pmc = json.loads((PROF / f"{tag}_pmc.json").read_text())
     r = bench["roofline"]
     print(f"bench: value {bench['value']} GiB/s, kernel {r['kernel_mean_ms'] * 1e3:.2f} us = {r['achieved']} GB/s "
