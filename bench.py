@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
-    ap.add_argument("--transports", default="xgmi,rccl", help="ring-leg transports, comma separated")
+    ap.add_argument("--transports", default="rccl,xgmi",
+                    help="ring-leg transports, comma separated (rccl first: the north-star P2P ring)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
