@@ -39,6 +39,18 @@ extern "C" {
  * reference's chunk_offsets() clamping (src/pg.c:126-138).  Elements. */
 PG_API int pg_block_range(int count, int world, int block, size_t *off, size_t *len);
 
+/* Rings.  With rings = 2 every block is split in two parts that travel in
+ * opposite directions, so both directions of each ring link carry data:
+ *   part 0 = [0, ceil(len/2)): clockwise (send to rank+1, receive from rank-1),
+ *            folded x[b+1] op x[b+2] op ... op x[b]   (indices mod world)
+ *   part 1 = [ceil(len/2), len): counter-clockwise (send to rank-1, receive
+ *            from rank+1), folded x[b-1] op x[b-2] op ... op x[b]
+ * rings = 1: one part, the whole block, clockwise.  Every transport (ring,
+ * eager one-shot, xgmi) folds each part in its ring's order, so all of them
+ * give identical bits for a given `rings` (PG_RINGS, default 2).  Elements. */
+#define PG_MAX_RINGS 2
+PG_API int pg_block_part(size_t len, int rings, int part, size_t *off, size_t *plen);
+
 /* Buffer roles named by plan steps. */
 #define PG_BUF_NONE   0
 #define PG_BUF_SRC    1   /* this rank's input (count elements)               */
@@ -46,10 +58,12 @@ PG_API int pg_block_range(int count, int world, int block, size_t *off, size_t *
 #define PG_BUF_STAGE0 3   /* HBM staging, one block                            */
 #define PG_BUF_STAGE1 4   /* HBM staging, one block                            */
 
-/* One ring step: in one transport group, send `send_bytes` to the right
- * neighbour and receive `recv_bytes` from the left; then (on the reduce
- * stream, after the receive) red_dst[i] = red_dst[i] op red_src[i] for
- * i < red_elems.  Offsets/lengths in bytes except red_elems. */
+/* One ring step: in one transport group, send `send_bytes` to rank
+ * (rank + send_peer) and receive `recv_bytes` from rank (rank + recv_peer),
+ * mod world (+1 / -1: the clockwise ring sends right and receives from the
+ * left, the counter-clockwise ring the opposite); then (on the reduce stream,
+ * after the receive) red_dst[i] = red_dst[i] op red_src[i] for i < red_elems.
+ * Offsets/lengths in bytes except red_elems. */
 struct pg_step {
   int32_t round;       /* ring round k, 0 .. world-2                          */
   int32_t batch;       /* steps with equal batch share one transport group    */
@@ -57,28 +71,35 @@ struct pg_step {
   int32_t send_wait;   /* 1: the sent segment is the previous round's reduce
                           output for `seg`; wait for it before sending        */
   int32_t send_buf, recv_buf, red_dst_buf, red_src_buf;
+  int32_t send_peer, recv_peer; /* rank offsets of the peers: +1 or -1      */
   int64_t send_off, send_bytes;
   int64_t recv_off, recv_bytes;
   int64_t red_dst_off, red_src_off, red_elems;
 };
 
-/* Reduce-scatter plan for one rank.  Round k sends block (rank-1-k) and
- * receives block (rank-2-k) mod world -- the reference's
+/* Reduce-scatter plan for one rank.  Clockwise ring: round k sends block
+ * (rank-1-k) and receives block (rank-2-k) mod world -- the reference's
  * rs_send/recv_chunk_index (src/pg.c:141-148) evaluated at rank-1, so that
- * rank r finishes with block r.  Segments: chunk_elems_from_bytes(chunk_bytes)
- * (src/pg.c:118-123) elements; blocks <= eager_max bytes are one segment;
- * `inflight` segments per batch.  out_aliases_src: OUT is block `rank` of
- * SRC (in-place all-reduce).  Returns the number of steps written (or needed,
- * when steps == NULL), -1 on bad arguments. */
+ * rank r finishes with block r.  Counter-clockwise ring (rings = 2): round k
+ * sends block (rank+1+k) and receives block (rank+2+k), its part 1 only.
+ * Segments: chunk_elems_from_bytes(chunk_bytes) (src/pg.c:118-123) elements;
+ * parts <= eager_max bytes are one segment; each batch carries `inflight`
+ * segment indices of every ring (clockwise steps first).  Ring 1 stages its
+ * parts at element ceil(B/2) of the staging blocks (B = ceil(count/world)).
+ * out_aliases_src: OUT is block `rank` of SRC (in-place all-reduce).  Returns
+ * the number of steps written (or needed, when steps == NULL), -1 on bad
+ * arguments. */
 PG_API int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
-                           size_t chunk_bytes, size_t eager_max, int inflight,
+                           size_t chunk_bytes, size_t eager_max, int inflight, int rings,
                            int out_aliases_src, struct pg_step *steps, int max_steps);
 
 /* All-gather plan: round k sends block (rank-k) and receives block
- * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole blocks, no reduce.
+ * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole parts, no reduce; with
+ * rings = 2 part 1 of each block goes the other way (round k sends block
+ * rank+k to rank-1 and receives block rank+k+1 from rank+1).
  * uniform = 1: blocks of `count` elements (pg_all_gather);
  * uniform = 0: the reduce-scatter partition of `count` (pg_all_reduce). */
-PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform,
+PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform, int rings,
                        struct pg_step *steps, int max_steps);
 
 /* Open a handle without a server list: transport LOOPBACK (reference mock
@@ -88,13 +109,14 @@ PG_API int pg_connect_local(int rank, int world, int transport, void **out_handl
 
 /* Run one collective over `world` virtual ranks in this process (transport
  * THREADS): rank r uses sendbufs[r] / recvbufs[r] (HIP device or host
- * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce. */
+ * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce.  rings: 1 or
+ * 2, 0 = PG_RINGS / the default. */
 #define PG_COLL_REDUCE_SCATTER 0
 #define PG_COLL_ALL_GATHER     1
 #define PG_COLL_ALL_REDUCE     2
 PG_API int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbufs,
                 int count, int datatype, int op, size_t chunk_bytes,
-                size_t eager_max, int inflight);
+                size_t eager_max, int inflight, int rings);
 
 /* The hot path with both operands in host memory: dst[i] = dst[i] op src[i]
  * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces (0 =

@@ -57,9 +57,11 @@ PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]
  * (k = nsrc; requires ceil(n / block_elems) <= k): block b folded in exactly
- * the order the ring reduce-scatter uses for it. */
+ * the order the ring reduce-scatter uses for it.  rings = 2: the second part
+ * of each block (position >= ceil(len_b/2), include/pg_ext.h) is folded
+ * srcs[(b-1)%k] op srcs[(b-2)%k] op ... op srcs[b] instead. */
 PG_API int pgk_fold_blocks(void *out, const void *const *srcs, int nsrc, size_t n, size_t block_elems,
-                           int dt, int op, void *stream);
+                           int rings, int dt, int op, void *stream);
 
 /* Copy k <= 16 byte ranges srcs[j] -> dsts[j] (bytes[j] each, 4-byte aligned,
  * sources may be peer memory) in one launch. */

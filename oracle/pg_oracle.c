@@ -138,18 +138,26 @@ void orc_ring_block(size_t count, int world, int b, size_t *off_elems, size_t *l
 }
 
 int orc_ring_reduce_scatter(int world, void *const *sends, void *const *outs,
-                            int count, int dt, int op) {
+                            int count, int dt, int op, int rings) {
     size_t es = orc_elem_size(dt);
-    if (world < 1 || count < 0 || es == 0) return -1;
+    if (world < 1 || count < 0 || es == 0 || rings < 1 || rings > 2) return -1;
     for (int b = 0; b < world; ++b) {
         size_t off, len;
         orc_ring_block((size_t)count, world, b, &off, &len);
         if (!len) continue;
-        char *acc = (char *)outs[b];
-        /* acc = x[b+1]; then acc = acc op x[b+j] for j = 2 .. world */
-        memcpy(acc, (const char *)sends[(b + 1) % world] + off * es, len * es);
-        for (int j = 2; j <= world; ++j)
-            orc_reduce_inplace(acc, (const char *)sends[(b + j) % world] + off * es, len, dt, op);
+        /* part 0 = [0, h): clockwise ring, acc = x[b+1]; acc = acc op x[b+j], j = 2 .. W
+         * part 1 = [h, len): counter-clockwise ring, x[b-1], x[b-2], ..., x[b]
+         * h = len for one ring, ceil(len/2) for two */
+        size_t h = rings == 1 ? len : (len + 1) / 2;
+        for (int g = 0; g < rings; ++g) {
+            size_t po = g == 0 ? 0 : h, pl = g == 0 ? h : len - h;
+            if (!pl) continue;
+            char *acc = (char *)outs[b] + po * es;
+            int step = g == 0 ? 1 : world - 1;
+            memcpy(acc, (const char *)sends[(b + step) % world] + (off + po) * es, pl * es);
+            for (int j = 2; j <= world; ++j)
+                orc_reduce_inplace(acc, (const char *)sends[(b + j * step) % world] + (off + po) * es, pl, dt, op);
+        }
     }
     return 0;
 }
@@ -166,7 +174,7 @@ int orc_ring_all_gather(int world, void *const *sends, void *const *recvs,
 }
 
 int orc_ring_all_reduce(int world, void *const *sends, void *const *recvs,
-                        int count, int dt, int op) {
+                        int count, int dt, int op, int rings) {
     size_t es = orc_elem_size(dt);
     if (world < 1 || count < 0 || es == 0) return -1;
     size_t total = (size_t)count * es;
@@ -178,7 +186,7 @@ int orc_ring_all_reduce(int world, void *const *sends, void *const *recvs,
         orc_ring_block((size_t)count, world, b, &off, &len);
         outs[b] = full + off * es;
     }
-    int rc = orc_ring_reduce_scatter(world, sends, outs, count, dt, op);
+    int rc = orc_ring_reduce_scatter(world, sends, outs, count, dt, op, rings);
     for (int r = 0; rc == 0 && r < world; ++r) memcpy(recvs[r], full, total);
     free(outs); free(full);
     return rc;

@@ -53,9 +53,9 @@ class Oracle:
             "orc_mock_reduce_scatter": (_I, [_I, _I, _SZ, _VP, _VP, _I, _I, _I]),
             "orc_mock_all_gather": (_I, [_I, _I, _VP, _VP, _I, _I]),
             "orc_mock_all_reduce": (_I, [_I, _I, _SZ, _VP, _VP, _I, _I, _I]),
-            "orc_ring_reduce_scatter": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I]),
+            "orc_ring_reduce_scatter": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _I]),
             "orc_ring_all_gather": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I]),
-            "orc_ring_all_reduce": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I]),
+            "orc_ring_all_reduce": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _I]),
             "orc_ring_block": (None, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
             "orc_fill": (None, [_VP, _SZ, _I, _I, ctypes.c_uint64]),
             "orc_time_reduce": (ctypes.c_double, [_VP, _VP, _SZ, _I, _I, _I]),
@@ -97,10 +97,11 @@ class Oracle:
         self.lib.orc_ring_block(count, world, b, ctypes.byref(off), ctypes.byref(ln))
         return off.value, ln.value
 
-    def ring_reduce_scatter(self, sends, dt, op):
+    # rings: 2 = the library default (PG_RINGS), 1 = one clockwise ring (include/pg_ext.h)
+    def ring_reduce_scatter(self, sends, dt, op, rings=2):
         world, count = len(sends), sends[0].size
         outs = [np.zeros(self.ring_block(count, world, b)[1], dtype=NP_DTYPE[dt]) for b in range(world)]
-        rc = self.lib.orc_ring_reduce_scatter(world, _ptr_array(sends), _ptr_array(outs), count, dt, op)
+        rc = self.lib.orc_ring_reduce_scatter(world, _ptr_array(sends), _ptr_array(outs), count, dt, op, rings)
         assert rc == 0
         return outs
 
@@ -111,10 +112,10 @@ class Oracle:
         assert rc == 0
         return recvs
 
-    def ring_all_reduce(self, sends, dt, op):
+    def ring_all_reduce(self, sends, dt, op, rings=2):
         world, count = len(sends), sends[0].size
         recvs = [np.zeros(count, dtype=NP_DTYPE[dt]) for _ in range(world)]
-        rc = self.lib.orc_ring_all_reduce(world, _ptr_array(sends), _ptr_array(recvs), count, dt, op)
+        rc = self.lib.orc_ring_all_reduce(world, _ptr_array(sends), _ptr_array(recvs), count, dt, op, rings)
         assert rc == 0
         return recvs
 

@@ -210,6 +210,12 @@ int pg_impl_create(struct pg *pg) {
   PG_CHECK_HIP(hipEventCreate(&im->t1));
   const char *e = getenv("PG_EAGER_ONESHOT");
   im->eager_oneshot = !(e && *e && atoi(e) == 0);
+  im->rings = 2;
+  e = getenv("PG_RINGS");
+  if (e && *e) {
+    im->rings = atoi(e);
+    if (im->rings < 1 || im->rings > PG_MAX_RINGS) { pg_set_error("PG_RINGS=%s: expected 1 or 2", e); return -1; }
+  }
   return 0;
 }
 
@@ -328,8 +334,8 @@ static int sync_ring(struct pg_impl *im, int timed) {
 static int plan_into(struct pg_impl *im, int is_rs, int count, int dt, int alias, int uniform) {
   struct pg *pg = im->pg;
   int n = is_rs ? pg_plan_reduce_scatter(pg->rank, pg->world_size, count, dt, pg->chunk_bytes,
-                                         pg->eager_max, pg->inflight, alias, NULL, 0)
-                : pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, NULL, 0);
+                                         pg->eager_max, pg->inflight, im->rings, alias, NULL, 0)
+                : pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, im->rings, NULL, 0);
   if (n < 0) { pg_set_error("plan: bad arguments"); return -1; }
   if (n > im->steps_cap) {
     struct pg_step *s = (struct pg_step *)realloc(im->steps, sizeof(*s) * (size_t)n);
@@ -339,9 +345,9 @@ static int plan_into(struct pg_impl *im, int is_rs, int count, int dt, int alias
   }
   if (is_rs)
     pg_plan_reduce_scatter(pg->rank, pg->world_size, count, dt, pg->chunk_bytes, pg->eager_max,
-                           pg->inflight, alias, im->steps, im->steps_cap);
+                           pg->inflight, im->rings, alias, im->steps, im->steps_cap);
   else
-    pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, im->steps, im->steps_cap);
+    pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, im->rings, im->steps, im->steps_cap);
   return n;
 }
 
@@ -386,32 +392,45 @@ static int upload_block(struct pg *pg, struct stage_ctx *c, int b) {
   return len ? pg_timed_copy(c->dev_src + off * es, c->host_src + off * es, len * es, c->h2d_us) : 0;
 }
 
-/* reduce-scatter rounds: round k reads source blocks r-1 (k = 0, sent) and r-2-k */
+/* reduce-scatter rounds: round k reads source blocks r-1 (k = 0, sent) and
+ * r-2-k; the counter-clockwise ring (rings = 2) reads r+1 and r+2+k */
 static int rs_upload_hook(struct pg_impl *im, void *ctx, int k) {
   struct pg *pg = im->pg;
   struct stage_ctx *c = (struct stage_ctx *)ctx;
   if (k >= pg->world_size - 1) return 0;
-  if (k == 0 && upload_block(pg, c, pg->rank - 1)) return -1;
-  if (upload_block(pg, c, pg->rank - 2 - k)) return -1;
-  if (k == 0 && upload_block(pg, c, pg->rank - 3)) return -1;   /* one block of lead */
+  for (int g = 0; g < im->rings; ++g) {
+    const int d = g == 0 ? -1 : 1;                                /* direction of the block walk */
+    if (k == 0 && upload_block(pg, c, pg->rank + d)) return -1;
+    if (upload_block(pg, c, pg->rank + d * (2 + k))) return -1;
+    if (k == 0 && upload_block(pg, c, pg->rank + d * 3)) return -1;   /* one block of lead */
+  }
   return 0;
 }
 
-/* all-gather rounds: round j receives block r-j-1.  Before round k starts,
- * every round < k has been enqueued; wait for the last recorded one (stream
- * order covers the earlier ones) and download the blocks of rounds
- * next_dl .. k-1.  Called with k = world-1 after the last round.  Rounds that
- * had no steps (empty blocks) have nothing to download. */
+/* all-gather rounds: the clockwise ring receives block r-j-1 in round j, the
+ * counter-clockwise one (rings = 2) block r+j+1, so block b is complete after
+ * round max((r-1-b) mod W, (b-r-1) mod W).  Before round k starts, every
+ * round < k has been enqueued; wait for the last recorded one (stream order
+ * covers the earlier ones) and download the blocks completed in rounds
+ * next_dl .. k-1.  Called with k = world-1 after the last round.  Empty
+ * blocks have nothing to download. */
 static int ag_download_hook(struct pg_impl *im, void *ctx, int k) {
   struct pg *pg = im->pg;
   struct stage_ctx *c = (struct stage_ctx *)ctx;
+  const int W = pg->world_size, r = pg->rank;
   if (!c->host_dst || c->next_dl >= k) return 0;
   if (im->last_round_rec >= 0) PG_CHECK_HIP(hipEventSynchronize(im->round_ev[im->last_round_rec]));
   size_t es = pg_elem_size(c->dt);
-  for (int j = c->next_dl; j < k; ++j) {
-    int b = ((pg->rank - j - 1) % pg->world_size + pg->world_size) % pg->world_size;
+  for (int b = 0; b < W; ++b) {
+    if (b == r) continue;
+    int done = ((r - 1 - b) % W + W) % W;
+    if (im->rings == 2) {
+      int j1 = ((b - r - 1) % W + W) % W;
+      if (j1 > done) done = j1;
+    }
+    if (done < c->next_dl || done >= k) continue;
     size_t off, len;
-    stage_block(c, pg->world_size, b, &off, &len);
+    stage_block(c, W, b, &off, &len);
     if (len && pg_timed_copy(c->host_dst + off * es, c->dev_dst + off * es, len * es, c->d2h_us)) return -1;
   }
   c->next_dl = k;
@@ -746,10 +765,6 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
 
 /* ---- host-memory reduce (the arriving-chunk step with host buffers) ------------ */
 
-/* dst[i] = dst[i] op src[i] with dst/src in host memory, staged through HBM
- * in pieces of chunk_bytes (default 256 MiB): threaded H2D of both operands
- * (pg_copy_parallel), the reduce, threaded D2H.  Measures the PCIe-inclusive
- * rate of the hot path. */
 /* ---- the chunk reduce with host operands (PCIe-inclusive path) ---------------
  *
  * dst and src live in host memory.  The buffers are cut into pieces that flow

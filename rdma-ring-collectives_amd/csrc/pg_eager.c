@@ -14,9 +14,10 @@
  *   all-reduce      every rank sends its whole input to every peer and
  *                   pgk_fold_blocks folds each block in its ring order.
  *
- * Fold order = the ring's (block b: x[b+1] op x[b+2] op ... op x[b], see
- * pg_plan.c and DESIGN.md §2), so results are bit-identical to the ring path
- * for int32 and double alike.  Used by the point-to-point transports (RCCL,
+ * Fold order = the ring's (block b: x[b+1] op x[b+2] op ... op x[b]; with two
+ * rings the second part of each block x[b-1] op x[b-2] op ... op x[b]; see
+ * pg_plan.c, include/pg_ext.h and DESIGN.md §2), so results are bit-identical
+ * to the ring path for int32 and double alike.  Used by the point-to-point transports (RCCL,
  * in-process threads) for W <= 16; xgmi has its own direct-read one-shot.
  * PG_EAGER_ONESHOT=0 turns it off.
  */
@@ -80,18 +81,22 @@ int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int cou
     im->stats.bytes_recv += (int64_t)slot;
   }
   if (im->ops->group_end(im, im->comm)) return -1;
-  if (blen) {
+  for (int g = 0; blen && g < im->rings; ++g) {     /* one launch per ring part of block r */
+    size_t po, pl;
+    pg_block_part(blen, im->rings, g, &po, &pl);
+    if (!pl) continue;
     const void *srcs[EAGER_MAX_WORLD];
     for (int j = 0; j < W; ++j) {
-      int q = (r + 1 + j) % W;                      /* ring order of block r */
-      srcs[j] = q == r ? (const void *)(src + boff * es) : (const void *)(gat + (size_t)q * slot);
+      int q = g == 0 ? (r + 1 + j) % W : ((r - 1 - j) % W + W) % W;   /* the part's ring order */
+      const char *base = q == r ? src + boff * es : gat + (size_t)q * slot;
+      srcs[j] = base + po * es;
     }
-    if (pgk_reduce_multi(out, srcs, W, blen, dt, op, (void *)im->comm)) {
+    if (pgk_reduce_multi(out + po * es, srcs, W, pl, dt, op, (void *)im->comm)) {
       pg_set_error("%s", pgk_last_error());
       return -1;
     }
     im->stats.reduce_launches++;
-    im->stats.reduce_elems += (int64_t)(blen * (size_t)(W - 1));
+    im->stats.reduce_elems += (int64_t)(pl * (size_t)(W - 1));
   }
   if (finish(im)) return -1;
   if (out != (char *)recvbuf && pg_timed_copy(recvbuf, out, slot, &im->stats.d2h_us)) return -1;
@@ -157,7 +162,7 @@ int pg_eager_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, 
   const void *srcs[EAGER_MAX_WORLD];
   for (int q = 0; q < W; ++q) srcs[q] = q == r ? (const void *)src : (const void *)(gat + (size_t)q * bytes);
   size_t blk = ((size_t)count + (size_t)W - 1) / (size_t)W;
-  if (pgk_fold_blocks(out, srcs, W, (size_t)count, blk, dt, op, (void *)im->comm)) {
+  if (pgk_fold_blocks(out, srcs, W, (size_t)count, blk, im->rings, dt, op, (void *)im->comm)) {
     pg_set_error("%s", pgk_last_error());
     return -1;
   }

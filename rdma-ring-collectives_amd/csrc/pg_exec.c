@@ -72,8 +72,7 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
     return hook ? hook(im, hook_ctx, pg_world_of(im) - 1) : 0;
   }
   const struct pg *pg = im->pg;
-  const int right = (pg->rank + 1) % pg->world_size;
-  const int left = (pg->rank - 1 + pg->world_size) % pg->world_size;
+  const int W = pg->world_size;
 
   int max_seg = 0;
   for (int i = 0; i < n; ++i) if (st[i].seg > max_seg) max_seg = st[i].seg;
@@ -102,13 +101,15 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
 
     if (im->ops->group_start(im)) return -1;
     for (int s = i; s < j; ++s) {
+      const int to = ((pg->rank + st[s].send_peer) % W + W) % W;
+      const int from = ((pg->rank + st[s].recv_peer) % W + W) % W;
       if (st[s].send_bytes &&
           im->ops->send(im, at(bufs, st[s].send_buf, st[s].send_off), (size_t)st[s].send_bytes,
-                        right, im->comm))
+                        to, im->comm))
         return -1;
       if (st[s].recv_bytes &&
           im->ops->recv(im, at(bufs, st[s].recv_buf, st[s].recv_off), (size_t)st[s].recv_bytes,
-                        left, im->comm))
+                        from, im->comm))
         return -1;
       im->stats.bytes_sent += st[s].send_bytes;
       im->stats.bytes_recv += st[s].recv_bytes;

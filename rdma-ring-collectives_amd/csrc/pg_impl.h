@@ -37,9 +37,10 @@
 
 struct pg_impl;
 
-/* The hop.  A group pairs the sends to the right neighbour with the receives
- * from the left neighbour of one batch; all are enqueued on `stream`.  Same
- * per-peer ordering rules as ncclSend/ncclRecv. */
+/* The hop.  A group holds the sends and receives of one batch (clockwise:
+ * to the right neighbour / from the left one; counter-clockwise: the
+ * opposite); all are enqueued on `stream`.  Same per-peer ordering rules as
+ * ncclSend/ncclRecv. */
 struct pg_xport_ops {
   const char *name;
   int (*group_start)(struct pg_impl *im);
@@ -69,6 +70,7 @@ struct pg_impl {
   void *dout;      size_t dout_cap;   /* device result / full buffer          */
   void *ebuf;      size_t ebuf_cap;   /* eager one-shot gather area (pg_eager.c) */
   int eager_oneshot;          /* PG_EAGER_ONESHOT, default 1                  */
+  int rings;                  /* PG_RINGS: 1 or 2 (default), pg_ext.h          */
 
   struct pg_step *steps; int steps_cap;
   int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */

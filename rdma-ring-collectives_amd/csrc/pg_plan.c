@@ -16,7 +16,11 @@
  *     (pg.h:127-139 "each rank receives an equal-sized chunk");
  *   - each round both sends and receives for real: send length and receive
  *     length are those of their own blocks (the mock used recv_len for both,
- *     src/pg.c:282-287).
+ *     src/pg.c:282-287);
+ *   - with rings = 2 (default) the second half of every block runs the mirror
+ *     schedule in the other direction, so both directions of each link carry
+ *     data (SURVEY.md §8f "bidirectional ring"); the reference's README
+ *     describes one ring (README.md:68-71).
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -54,94 +58,150 @@ static size_t seg_elems_for(size_t len, size_t es, size_t chunk_bytes, size_t ea
 
 static size_t nsegs(size_t len, size_t seg) { return len ? (len + seg - 1) / seg : 0; }
 
+int pg_block_part(size_t len, int rings, int part, size_t *off, size_t *plen) {
+  if (rings < 1 || rings > PG_MAX_RINGS || part < 0 || part >= rings || !off || !plen) return -1;
+  size_t h = rings == 1 ? len : (len + 1) / 2;
+  *off = part == 0 ? 0 : h;
+  *plen = part == 0 ? h : len - h;
+  return 0;
+}
+
 static void put(struct pg_step *steps, int max_steps, int n, const struct pg_step *s) {
   if (steps && n < max_steps) steps[n] = *s;
 }
 
+/* One ring's view of round k: the blocks it sends and receives (this rank's
+ * parts of them) and how they are cut into segments. */
+struct ring_round {
+  int dir;                      /* +1 clockwise, -1 counter-clockwise       */
+  size_t so, sl, to, tl;        /* sent / received block: offset, length    */
+  size_t sp, spl, tp, tpl;      /* this ring's part of each: offset, length */
+  size_t sseg, tseg, ns, nt;    /* segment lengths and counts               */
+  size_t stage_base;            /* element offset of this ring in staging   */
+  int seg_base;                 /* first event slot of this ring            */
+};
+
 int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
-                           size_t chunk_bytes, size_t eager_max, int inflight,
+                           size_t chunk_bytes, size_t eager_max, int inflight, int rings,
                            int out_aliases_src, struct pg_step *steps, int max_steps) {
   size_t es = plan_elem_size(datatype);
-  if (!es || world < 1 || rank < 0 || rank >= world || count < 0) return -1;
+  if (!es || world < 1 || rank < 0 || rank >= world || count < 0 || rings < 1 || rings > PG_MAX_RINGS) return -1;
   if (inflight < 1) inflight = 1;
+  size_t bfull = ((size_t)count + (size_t)world - 1) / (size_t)world;
+  size_t bh, bhl;
+  pg_block_part(bfull, rings, 0, &bh, &bhl);         /* part 0 of a full block: the largest part */
+  int seg_stride = (int)nsegs(bhl, seg_elems_for(bhl, es, chunk_bytes, eager_max));
   int n = 0, batch = -1;
   for (int k = 0; k + 1 < world; ++k) {
-    int sb = ring_mod(rank - 1 - k, world);   /* rs_send_chunk_index(k, rank-1) */
-    int tb = ring_mod(rank - 2 - k, world);   /* rs_recv_chunk_index(k, rank-1) */
-    size_t so, sl, to, tl;
-    pg_block_range(count, world, sb, &so, &sl);
-    pg_block_range(count, world, tb, &to, &tl);
-    int last = (k == world - 2);
-    size_t sseg = seg_elems_for(sl, es, chunk_bytes, eager_max);
-    size_t tseg = seg_elems_for(tl, es, chunk_bytes, eager_max);
-    size_t ns = nsegs(sl, sseg), nt = nsegs(tl, tseg);
-    size_t nj = ns > nt ? ns : nt;
-    int in_batch = inflight;                  /* force a new batch per round */
-    for (size_t j = 0; j < nj; ++j) {
-      struct pg_step st;
-      memset(&st, 0, sizeof(st));
-      if (in_batch == inflight) { ++batch; in_batch = 0; }
-      ++in_batch;
-      st.round = k;
-      st.batch = batch;
-      st.seg = (int32_t)j;
-      if (j < ns) {
-        size_t e0 = j * sseg, len = sl - e0 < sseg ? sl - e0 : sseg;
-        if (k == 0) { st.send_buf = PG_BUF_SRC; st.send_off = (int64_t)((so + e0) * es); }
-        else {
-          st.send_buf = ((k - 1) & 1) ? PG_BUF_STAGE1 : PG_BUF_STAGE0;
-          st.send_off = (int64_t)(e0 * es);
-          st.send_wait = 1;                   /* previous round reduced it */
+    const int last = (k == world - 2);
+    struct ring_round rr[PG_MAX_RINGS];
+    size_t nj = 0;
+    for (int g = 0; g < rings; ++g) {
+      struct ring_round *q = &rr[g];
+      q->dir = g == 0 ? 1 : -1;
+      /* clockwise: rs_send/recv_chunk_index(k, rank-1); counter-clockwise: the mirror */
+      int sb = g == 0 ? ring_mod(rank - 1 - k, world) : ring_mod(rank + 1 + k, world);
+      int tb = g == 0 ? ring_mod(rank - 2 - k, world) : ring_mod(rank + 2 + k, world);
+      pg_block_range(count, world, sb, &q->so, &q->sl);
+      pg_block_range(count, world, tb, &q->to, &q->tl);
+      pg_block_part(q->sl, rings, g, &q->sp, &q->spl);
+      pg_block_part(q->tl, rings, g, &q->tp, &q->tpl);
+      q->sseg = seg_elems_for(q->spl, es, chunk_bytes, eager_max);
+      q->tseg = seg_elems_for(q->tpl, es, chunk_bytes, eager_max);
+      q->ns = nsegs(q->spl, q->sseg);
+      q->nt = nsegs(q->tpl, q->tseg);
+      q->stage_base = g == 0 ? 0 : (bfull + 1) / 2;
+      q->seg_base = g * seg_stride;
+      size_t m = q->ns > q->nt ? q->ns : q->nt;
+      if (m > nj) nj = m;
+    }
+    /* batches: segment indices [j0, j0 + inflight) of every ring, clockwise first */
+    for (size_t j0 = 0; j0 < nj; j0 += (size_t)inflight) {
+      ++batch;
+      size_t j1 = j0 + (size_t)inflight < nj ? j0 + (size_t)inflight : nj;
+      for (int g = 0; g < rings; ++g) {
+        const struct ring_round *q = &rr[g];
+        for (size_t j = j0; j < j1; ++j) {
+          if (j >= q->ns && j >= q->nt) continue;
+          struct pg_step st;
+          memset(&st, 0, sizeof(st));
+          st.round = k;
+          st.batch = batch;
+          st.seg = q->seg_base + (int32_t)j;
+          st.send_peer = q->dir;
+          st.recv_peer = -q->dir;
+          if (j < q->ns) {
+            size_t e0 = j * q->sseg, len = q->spl - e0 < q->sseg ? q->spl - e0 : q->sseg;
+            if (k == 0) { st.send_buf = PG_BUF_SRC; st.send_off = (int64_t)((q->so + q->sp + e0) * es); }
+            else {
+              st.send_buf = ((k - 1) & 1) ? PG_BUF_STAGE1 : PG_BUF_STAGE0;
+              st.send_off = (int64_t)((q->stage_base + e0) * es);
+              st.send_wait = 1;                 /* previous round reduced it */
+            }
+            st.send_bytes = (int64_t)(len * es);
+          }
+          if (j < q->nt) {
+            size_t e0 = j * q->tseg, len = q->tpl - e0 < q->tseg ? q->tpl - e0 : q->tseg;
+            int stage = (k & 1) ? PG_BUF_STAGE1 : PG_BUF_STAGE0;
+            int64_t stage_off = (int64_t)((q->stage_base + e0) * es);
+            if (last && !out_aliases_src) {
+              st.recv_buf = PG_BUF_OUT;
+              st.recv_off = (int64_t)((q->tp + e0) * es);
+            } else {
+              st.recv_buf = stage;
+              st.recv_off = stage_off;
+            }
+            st.recv_bytes = (int64_t)(len * es);
+            st.red_elems = (int64_t)len;
+            if (last && out_aliases_src) {
+              /* OUT is block `rank` of SRC: fold the arrival into it in place
+               * (local op incoming == incoming op local bit for bit: + and * are
+               * commutative in IEEE-754 and in two's complement) */
+              st.red_dst_buf = PG_BUF_OUT; st.red_dst_off = (int64_t)((q->tp + e0) * es);
+              st.red_src_buf = stage;      st.red_src_off = stage_off;
+            } else {
+              /* arrival op= this rank's own contribution to the block */
+              st.red_dst_buf = st.recv_buf; st.red_dst_off = st.recv_off;
+              st.red_src_buf = PG_BUF_SRC;  st.red_src_off = (int64_t)((q->to + q->tp + e0) * es);
+            }
+          }
+          put(steps, max_steps, n, &st);
+          ++n;
         }
-        st.send_bytes = (int64_t)(len * es);
       }
-      if (j < nt) {
-        size_t e0 = j * tseg, len = tl - e0 < tseg ? tl - e0 : tseg;
-        int stage = (k & 1) ? PG_BUF_STAGE1 : PG_BUF_STAGE0;
-        st.recv_buf = (last && !out_aliases_src) ? PG_BUF_OUT : stage;
-        st.recv_off = (int64_t)(e0 * es);
-        st.recv_bytes = (int64_t)(len * es);
-        st.red_elems = (int64_t)len;
-        if (last && out_aliases_src) {
-          /* OUT is block `rank` of SRC: fold the arrival into it in place
-           * (local op incoming == incoming op local bit for bit: + and * are
-           * commutative in IEEE-754 and in two's complement) */
-          st.red_dst_buf = PG_BUF_OUT; st.red_dst_off = st.recv_off;
-          st.red_src_buf = stage;      st.red_src_off = st.recv_off;
-        } else {
-          /* arrival op= this rank's own contribution to the block */
-          st.red_dst_buf = st.recv_buf; st.red_dst_off = st.recv_off;
-          st.red_src_buf = PG_BUF_SRC;  st.red_src_off = (int64_t)((to + e0) * es);
-        }
-      }
-      put(steps, max_steps, n, &st);
-      ++n;
     }
   }
   if (steps && n > max_steps) return -1;
   return n;
 }
 
-int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform,
+int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform, int rings,
                        struct pg_step *steps, int max_steps) {
   size_t es = plan_elem_size(datatype);
-  if (!es || world < 1 || rank < 0 || rank >= world || count < 0) return -1;
+  if (!es || world < 1 || rank < 0 || rank >= world || count < 0 || rings < 1 || rings > PG_MAX_RINGS) return -1;
   int n = 0;
   for (int k = 0; k + 1 < world; ++k) {
-    int sb = ring_mod(rank - k, world);       /* src/pg.c:310 */
-    int rb = ring_mod(rank - k - 1, world);   /* src/pg.c:311 */
-    size_t so, sl, ro, rl;
-    if (uniform) { so = (size_t)sb * (size_t)count; sl = (size_t)count; ro = (size_t)rb * (size_t)count; rl = (size_t)count; }
-    else { pg_block_range(count, world, sb, &so, &sl); pg_block_range(count, world, rb, &ro, &rl); }
-    if (!sl && !rl) continue;
-    struct pg_step st;
-    memset(&st, 0, sizeof(st));
-    st.round = k;
-    st.batch = k;
-    if (sl) { st.send_buf = PG_BUF_OUT; st.send_off = (int64_t)(so * es); st.send_bytes = (int64_t)(sl * es); }
-    if (rl) { st.recv_buf = PG_BUF_OUT; st.recv_off = (int64_t)(ro * es); st.recv_bytes = (int64_t)(rl * es); }
-    put(steps, max_steps, n, &st);
-    ++n;
+    for (int g = 0; g < rings; ++g) {
+      int sb = g == 0 ? ring_mod(rank - k, world) : ring_mod(rank + k, world);          /* src/pg.c:310 */
+      int rb = g == 0 ? ring_mod(rank - k - 1, world) : ring_mod(rank + k + 1, world);  /* src/pg.c:311 */
+      size_t so, sl, ro, rl, sp, spl, rp, rpl;
+      if (uniform) { so = (size_t)sb * (size_t)count; sl = (size_t)count; ro = (size_t)rb * (size_t)count; rl = (size_t)count; }
+      else { pg_block_range(count, world, sb, &so, &sl); pg_block_range(count, world, rb, &ro, &rl); }
+      pg_block_part(sl, rings, g, &sp, &spl);
+      pg_block_part(rl, rings, g, &rp, &rpl);
+      if (!spl && !rpl) continue;
+      struct pg_step st;
+      memset(&st, 0, sizeof(st));
+      st.round = k;
+      st.batch = k;
+      st.seg = g;
+      st.send_peer = g == 0 ? 1 : -1;
+      st.recv_peer = -st.send_peer;
+      if (spl) { st.send_buf = PG_BUF_OUT; st.send_off = (int64_t)((so + sp) * es); st.send_bytes = (int64_t)(spl * es); }
+      if (rpl) { st.recv_buf = PG_BUF_OUT; st.recv_off = (int64_t)((ro + rp) * es); st.recv_bytes = (int64_t)(rpl * es); }
+      put(steps, max_steps, n, &st);
+      ++n;
+    }
   }
   if (steps && n > max_steps) return -1;
   return n;

@@ -204,8 +204,11 @@ static void *sim_thread(void *arg) {
 
 int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbufs,
                 int count, int datatype, int op, size_t chunk_bytes,
-                size_t eager_max, int inflight) {
-  if (world < 1 || world > 64 || !recvbufs || coll < 0 || coll > 2) { pg_set_error("pgx_sim_run: bad arguments"); return -1; }
+                size_t eager_max, int inflight, int rings) {
+  if (world < 1 || world > 64 || !recvbufs || coll < 0 || coll > 2 || rings < 0 || rings > PG_MAX_RINGS) {
+    pg_set_error("pgx_sim_run: bad arguments");
+    return -1;
+  }
   int dev = 0;
   PG_CHECK_HIP(hipGetDevice(&dev));
   struct sim_hub hub;
@@ -232,6 +235,7 @@ int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *recvbuf
     pg->transport = world == 1 ? PG_TRANSPORT_SELF : PG_TRANSPORT_THREADS;
     jobs[r].pg = pg;
     if (pg_impl_create(pg) || pg_xport_threads_attach(pg, &hub)) goto out;
+    if (rings) ((struct pg_impl *)pg->impl)->rings = rings;    /* 0: PG_RINGS / default */
     jobs[r].device = dev; jobs[r].coll = coll; jobs[r].count = count;
     jobs[r].dt = datatype; jobs[r].op = op;
     jobs[r].send = sendbufs ? sendbufs[r] : NULL;

@@ -374,20 +374,30 @@ static int finish(struct pg *pg, int zero_copy, int fail) {
   return (rc || fail) ? -1 : 0;
 }
 
-/* out = fold over ranks, in ring order, of the block at off_elems. */
+/* out = fold over ranks of this rank's block (at off_elems, len elements),
+ * each ring part in its ring's order (include/pg_ext.h): bit-identical to the
+ * P2P ring with the same PG_RINGS. */
 static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size_t off_elems, size_t len, int dt,
                       int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   if (!len) return 0;
   int W = pg->world_size, r = pg->rank;
   size_t es = pg_elem_size(dt);
-  const void *srcs[16];
-  for (int j = 0; j < W; ++j) srcs[j] = by_rank[(r + 1 + j) % W] + off_elems * es;
   double tk = us_now();
   pg_trace(pg, "xgmi fold: %zu elements from %d ranks", len, W);
-  if (pgk_reduce_multi(out, srcs, W, len, dt, op, (void *)im->red)) {
-    pg_set_error("xgmi: %s", pgk_last_error());
-    return -1;
+  for (int g = 0; g < im->rings; ++g) {
+    size_t po, pl;
+    pg_block_part(len, im->rings, g, &po, &pl);
+    if (!pl) continue;
+    const void *srcs[16];
+    for (int j = 0; j < W; ++j) {
+      int q = g == 0 ? (r + 1 + j) % W : ((r - 1 - j) % W + W) % W;
+      srcs[j] = by_rank[q] + (off_elems + po) * es;
+    }
+    if (pgk_reduce_multi((char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red)) {
+      pg_set_error("xgmi: %s", pgk_last_error());
+      return -1;
+    }
   }
   if (pg_stream_wait(im->red)) return -1;
   pg_trace(pg, "xgmi fold: done");
@@ -494,7 +504,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
       for (int q = 0; q < pg->world_size; ++q) srcs[q] = by_rank[q];
       size_t blk = ((size_t)count + (size_t)pg->world_size - 1) / (size_t)pg->world_size;
       double tk = us_now();
-      if (pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, dt, op, (void *)im->red) ||
+      if (pgk_fold_blocks(full, srcs, pg->world_size, (size_t)count, blk, im->rings, dt, op, (void *)im->red) ||
           pg_stream_wait(im->red)) {
         pg_set_error("xgmi: %s", pgk_last_error());
         fail = 1;

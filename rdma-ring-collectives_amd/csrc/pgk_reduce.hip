@@ -171,17 +171,22 @@ __global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_scalar(T* __restri
 // and is folded in that block's ring order, src[(b+1)%k] op src[(b+2)%k] ...
 // op src[b] -- the order the reduce-scatter uses for block b, so every rank
 // computing the whole vector this way gets the all-reduce result bit for bit.
+// With two rings the second part of a block (position >= ceil(len_b / 2))
+// travels the other way and folds src[(b-1)%k] op src[(b-2)%k] ... op src[b].
 // Used for small messages, where one launch beats reduce-scatter + gather.
 template <typename T, int OP>
 __global__ __launch_bounds__(kMultiBlock) void k_fold_blocks(T* __restrict__ out, SrcList<T> src, int k,
-                                                             size_t n, size_t block_elems) {
+                                                             size_t n, size_t block_elems, int rings) {
   const size_t stride = (size_t)gridDim.x * kMultiBlock;
   for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < n; i += stride) {
-    int b = (int)(i / block_elems);
-    int q = b + 1 >= k ? b + 1 - k : b + 1;
+    const int b = (int)(i / block_elems);
+    const size_t b0 = (size_t)b * block_elems;
+    const size_t len = n - b0 < block_elems ? n - b0 : block_elems;
+    const int step = (rings == 2 && i - b0 >= (len + 1) / 2) ? k - 1 : 1;   // -1 mod k
+    int q = b + step >= k ? b + step - k : b + step;
     T acc = src.p[q][i];
     for (int j = 1; j < k; ++j) {
-      q = q + 1 == k ? 0 : q + 1;
+      q = q + step >= k ? q + step - k : q + step;
       acc = apply<OP>(acc, src.p[q][i]);
     }
     out[i] = acc;
@@ -432,11 +437,12 @@ int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int
 }
 
 
-int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size_t block_elems, int dt, int op,
-                    void* stream) {
+int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size_t block_elems, int rings,
+                    int dt, int op, void* stream) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
+  if (rings != 1 && rings != 2) { set_err("pgk: rings %d, expected 1 or 2", rings); return -1; }
   if (n == 0) return 0;
   if (!out || !srcs || block_elems == 0 || (n + block_elems - 1) / block_elems > (size_t)nsrc) {
     set_err("pgk: bad fold_blocks arguments");
@@ -450,19 +456,19 @@ int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size
     for (int j = 0; j < nsrc; ++j) sl.p[j] = (const uint32_t*)srcs[j];
     if (op == PGK_OP_SUM)
       hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (uint32_t*)out, sl, nsrc, n, block_elems);
+                         (uint32_t*)out, sl, nsrc, n, block_elems, rings);
     else
       hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (uint32_t*)out, sl, nsrc, n, block_elems);
+                         (uint32_t*)out, sl, nsrc, n, block_elems, rings);
   } else {
     SrcList<double> sl{};
     for (int j = 0; j < nsrc; ++j) sl.p[j] = (const double*)srcs[j];
     if (op == PGK_OP_SUM)
       hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (double*)out, sl, nsrc, n, block_elems);
+                         (double*)out, sl, nsrc, n, block_elems, rings);
     else
       hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (double*)out, sl, nsrc, n, block_elems);
+                         (double*)out, sl, nsrc, n, block_elems, rings);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }

@@ -36,6 +36,7 @@ class PgStep(ctypes.Structure):
         ("send_wait", ctypes.c_int32),
         ("send_buf", ctypes.c_int32), ("recv_buf", ctypes.c_int32),
         ("red_dst_buf", ctypes.c_int32), ("red_src_buf", ctypes.c_int32),
+        ("send_peer", ctypes.c_int32), ("recv_peer", ctypes.c_int32),
         ("send_off", ctypes.c_int64), ("send_bytes", ctypes.c_int64),
         ("recv_off", ctypes.c_int64), ("recv_bytes", ctypes.c_int64),
         ("red_dst_off", ctypes.c_int64), ("red_src_off", ctypes.c_int64),
@@ -81,10 +82,11 @@ _SIGS = {
     "pg_all_gather": (_I, [_VP, _VP, _I, _I, _VP]),
     # include/pg_ext.h
     "pg_block_range": (_I, [_I, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
-    "pg_plan_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _SZ, _I, _I, ctypes.POINTER(PgStep), _I]),
-    "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_plan_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _SZ, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_block_part": (_I, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "pg_connect_local": (_I, [_I, _I, _I, ctypes.POINTER(_VP)]),
-    "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I]),
+    "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I, _I]),
     "pg_get_stats": (_I, [_VP, ctypes.POINTER(PgStats)]),
     "pgx_reduce_host": (_I, [_VP, _CVP, _SZ, _I, _I, _SZ]),
     "pg_last_error": (ctypes.c_char_p, []),
@@ -93,7 +95,7 @@ _SIGS = {
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
-    "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _VP]),
+    "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),
     "pgk_device_count": (_I, [ctypes.POINTER(_I)]),
     "pgk_set_device": (_I, [_I]),
@@ -151,24 +153,32 @@ def block_range(count: int, world: int, block: int) -> tuple[int, int]:
     return off.value, ln.value
 
 
-def plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max=4096, inflight=4, alias=0):
+def block_part(length: int, rings: int, part: int) -> tuple[int, int]:
+    """(offset, length) of ring part `part` of a block (include/pg_ext.h)."""
     lib = load()
-    n = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, alias, None, 0)
+    off, ln = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib.pg_block_part(length, rings, part, ctypes.byref(off), ctypes.byref(ln)), "pg_block_part")
+    return off.value, ln.value
+
+
+def plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max=4096, inflight=4, alias=0, rings=2):
+    lib = load()
+    n = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, rings, alias, None, 0)
     if n < 0:
         raise ValueError("pg_plan_reduce_scatter: bad arguments")
     arr = (PgStep * max(n, 1))()
-    m = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, alias, arr, n)
+    m = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, rings, alias, arr, n)
     assert m == n
     return [arr[i].as_dict() for i in range(n)]
 
 
-def plan_all_gather(rank, world, count, dt, uniform=1):
+def plan_all_gather(rank, world, count, dt, uniform=1, rings=2):
     lib = load()
-    n = lib.pg_plan_all_gather(rank, world, count, dt, uniform, None, 0)
+    n = lib.pg_plan_all_gather(rank, world, count, dt, uniform, rings, None, 0)
     if n < 0:
         raise ValueError("pg_plan_all_gather: bad arguments")
     arr = (PgStep * max(n, 1))()
-    lib.pg_plan_all_gather(rank, world, count, dt, uniform, arr, n)
+    lib.pg_plan_all_gather(rank, world, count, dt, uniform, rings, arr, n)
     return [arr[i].as_dict() for i in range(n)]
 
 

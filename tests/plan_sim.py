@@ -3,7 +3,9 @@
 Used to check the HOST SCHEDULE without a GPU: each rank's plan -- produced by
 the library's pg_plan_* C functions -- is executed with per-edge FIFO channels
 (the semantics of ncclSend/ncclRecv between ring neighbours) and the reduction
-is done here with numpy's wrapping/IEEE arithmetic.  This file is test
+is done here with numpy's wrapping/IEEE arithmetic.  A step sends to rank
+(r + send_peer) and receives from rank (r + recv_peer), one FIFO per directed
+edge, so both ring directions are simulated.  This file is test
 infrastructure; nothing in the library calls it.
 """
 from __future__ import annotations
@@ -42,7 +44,7 @@ def run_plans(plans, bufs_per_rank, dt, op):
     at send time (a rank's steps run in order, so a forwarded partial is
     already reduced, as the executor's red_ev wait guarantees)."""
     world = len(plans)
-    chans = [deque() for _ in range(world)]     # chans[r]: r -> r+1
+    chans = {(a, b): deque() for a in range(world) for b in range(world)}     # directed edge a -> b
     pos = [0] * world
     # group steps into batches per rank
     batches = []
@@ -67,16 +69,20 @@ def run_plans(plans, bufs_per_rank, dt, op):
             if pending[r] is None:
                 for s in batch:
                     if s["send_bytes"]:
-                        chans[r].append(_view(bufs, s["send_buf"], s["send_off"], s["send_bytes"]).copy())
+                        chans[(r, (r + s["send_peer"]) % world)].append(
+                            _view(bufs, s["send_buf"], s["send_off"], s["send_bytes"]).copy())
                 pending[r] = True
                 progress = True
-            left = chans[(r - 1) % world]
-            need = sum(1 for s in batch if s["recv_bytes"])
-            if len(left) < need:
+            need = {}
+            for s in batch:
+                if s["recv_bytes"]:
+                    q = (r + s["recv_peer"]) % world
+                    need[q] = need.get(q, 0) + 1
+            if any(len(chans[(q, r)]) < k for q, k in need.items()):
                 continue
             for s in batch:
                 if s["recv_bytes"]:
-                    msg = left.popleft()
+                    msg = chans[((r + s["recv_peer"]) % world, r)].popleft()
                     assert msg.size == s["recv_bytes"], (r, s, msg.size)
                     _view(bufs, s["recv_buf"], s["recv_off"], s["recv_bytes"])[:] = msg
             for s in batch:
@@ -88,16 +94,17 @@ def run_plans(plans, bufs_per_rank, dt, op):
             pending[r] = None
             progress = True
     assert all(pos[r] == len(batches[r]) for r in range(world)), "deadlock"
-    assert all(len(c) == 0 for c in chans), "unconsumed messages"
+    assert all(len(c) == 0 for c in chans.values()), "unconsumed messages"
 
 
-def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False):
+def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False, rings=2):
     world, count = len(sends), sends[0].size
     es = 4 if dt == 0 else 8
     bmax = -(-count // world) * es if count else 0
     plans, bufs = [], []
     for r in range(world):
-        plans.append(pgamd.plan_reduce_scatter(r, world, count, dt, chunk_bytes, eager_max, inflight, int(alias)))
+        plans.append(pgamd.plan_reduce_scatter(r, world, count, dt, chunk_bytes, eager_max, inflight, int(alias),
+                                               rings))
         off, ln = pgamd.block_range(count, world, r)
         src = sends[r].copy().view(np.uint8)
         if alias:
@@ -110,12 +117,12 @@ def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, 
     return [bufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)], bufs
 
 
-def ring_all_gather(sends, dt):
+def ring_all_gather(sends, dt, rings=2):
     world, count = len(sends), sends[0].size
     es = 4 if dt == 0 else 8
     plans, bufs = [], []
     for r in range(world):
-        plans.append(pgamd.plan_all_gather(r, world, count, dt, 1))
+        plans.append(pgamd.plan_all_gather(r, world, count, dt, 1, rings))
         full = np.zeros(count * world * es, np.uint8)
         full[r * count * es:(r + 1) * count * es] = sends[r].view(np.uint8)
         bufs.append({pgamd.PG_BUF_OUT: full})
@@ -123,10 +130,10 @@ def ring_all_gather(sends, dt):
     return [b[pgamd.PG_BUF_OUT].view(NP[dt]).copy() for b in bufs]
 
 
-def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4):
+def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, rings=2):
     world, count = len(sends), sends[0].size
-    _, bufs = ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max, inflight, alias=True)
-    plans = [pgamd.plan_all_gather(r, world, count, dt, 0) for r in range(world)]
+    _, bufs = ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max, inflight, alias=True, rings=rings)
+    plans = [pgamd.plan_all_gather(r, world, count, dt, 0, rings) for r in range(world)]
     agbufs = [{pgamd.PG_BUF_OUT: bufs[r][pgamd.PG_BUF_SRC]} for r in range(world)]
     run_plans(plans, agbufs, dt, 0)
     return [agbufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)]

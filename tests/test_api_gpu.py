@@ -177,7 +177,7 @@ def test_loopback_mock_all_gather_and_refusals(gpu, lib, golden):
             lib.pg_close(h)
 
 
-def sim(lib, torch, coll, sends, recvs, count, dt, op, chunk_bytes, eager_max, inflight, on_dev):
+def sim(lib, torch, coll, sends, recvs, count, dt, op, chunk_bytes, eager_max, inflight, on_dev, rings=2):
     world = len(sends)
     if on_dev:
         S = [to_dev(torch, s) for s in sends]
@@ -189,7 +189,7 @@ def sim(lib, torch, coll, sends, recvs, count, dt, op, chunk_bytes, eager_max, i
         R = [r.copy() for r in recvs]
         sp = (ctypes.c_void_p * world)(*[s.ctypes.data for s in S])
         rp = (ctypes.c_void_p * world)(*[r.ctypes.data for r in R])
-    rc = lib.pgx_sim_run(world, coll, sp, rp, count, dt, op, chunk_bytes, eager_max, inflight)
+    rc = lib.pgx_sim_run(world, coll, sp, rp, count, dt, op, chunk_bytes, eager_max, inflight, rings)
     assert rc == 0, pgamd.last_error()
     return [to_host(torch, r) if on_dev else r for r in R]
 
@@ -204,53 +204,56 @@ CASES = [  # world, dt, op, count, chunk_bytes, eager_max, inflight
 ]
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("case", CASES)
-def test_ring_reduce_scatter_sim(gpu, lib, oracle, case):
+def test_ring_reduce_scatter_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count, cb, eager, infl = case
     xs = [oracle.fill(count, dt, op, 1000 + 7 * r + count) for r in range(world)]
-    want = oracle.ring_reduce_scatter(xs, dt, op)
+    want = oracle.ring_reduce_scatter(xs, dt, op, rings)
     for on_dev in (True, False):
         recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want]
-        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, cb, eager, infl, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, cb, eager, infl, on_dev, rings)
         for r in range(world):
             assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (case, r, on_dev)
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("case", CASES)
-def test_ring_all_reduce_sim(gpu, lib, oracle, case):
+def test_ring_all_reduce_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count, cb, eager, infl = case
     xs = [oracle.fill(count, dt, op, 2000 + 3 * r + count) for r in range(world)]
-    want = oracle.ring_all_reduce(xs, dt, op)
+    want = oracle.ring_all_reduce(xs, dt, op, rings)
     for on_dev, in_place in itertools.product((True, False), (False, True)):
         recvs = [x.copy() if in_place else np.zeros(count, NP[dt]) for x in xs]
         if in_place:
             torch = gpu
             R = [to_dev(torch, r) for r in recvs] if on_dev else recvs
             ps = (ctypes.c_void_p * world)(*[(ptr(r) if on_dev else r.ctypes.data) for r in R])
-            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, cb, eager, infl) == 0, \
-                pgamd.last_error()
+            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, cb, eager, infl,
+                                   rings) == 0, pgamd.last_error()
             got = [to_host(torch, r) if on_dev else r for r in R]
         else:
-            got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, recvs, count, dt, op, cb, eager, infl, on_dev)
+            got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, recvs, count, dt, op, cb, eager, infl, on_dev, rings)
         for r in range(world):
             assert got[r].tobytes() == want[r].tobytes(), (case, r, on_dev, in_place)
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("world,count", [(2, 1), (3, 1000), (4, 0), (8, 4099)])
-def test_ring_all_gather_sim(gpu, lib, oracle, world, count):
+def test_ring_all_gather_sim(gpu, lib, oracle, world, count, rings):
     for dt in (0, 1):
         xs = [oracle.fill(count, dt, 0, 3000 + r) for r in range(world)]
         want = oracle.ring_all_gather(xs, dt)
         for on_dev in (True, False):
             recvs = [np.zeros(count * world, NP[dt]) for _ in range(world)]
-            got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, recvs, count, dt, 0, 4096, 0, 1, on_dev)
+            got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, recvs, count, dt, 0, 4096, 0, 1, on_dev, rings)
             for r in range(world):
                 assert got[r].tobytes() == want[r].tobytes()
 
 
 def test_ring_large_device_resident(gpu, lib, oracle):
     """A 4-rank, 64 Mi-element double sum (512 MiB per rank) with 4 MiB
-    segments: bit-exact against the oracle."""
+    segments, two rings: bit-exact against the oracle."""
     torch = gpu
     world, count, dt, op = 4, 1 << 26, 1, 0
     xs = [oracle.fill(count, dt, op, 4000 + r) for r in range(world)]
@@ -271,37 +274,39 @@ EAGER_CASES = [  # world, dt, op, count   (eager_max = 4096 bytes)
 ]
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("case", EAGER_CASES)
-def test_eager_oneshot_sim(gpu, lib, oracle, case):
+def test_eager_oneshot_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count = case
     xs = [oracle.fill(count, dt, op, 5000 + 11 * r + count) for r in range(world)]
-    want_rs = oracle.ring_reduce_scatter(xs, dt, op)
-    want_ar = oracle.ring_all_reduce(xs, dt, op)
+    want_rs = oracle.ring_reduce_scatter(xs, dt, op, rings)
+    want_ar = oracle.ring_all_reduce(xs, dt, op, rings)
     want_ag = oracle.ring_all_gather(xs, dt)
     for on_dev in (True, False):
         recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want_rs]
-        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, 0, 4096, 4, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, recvs, count, dt, op, 0, 4096, 4, on_dev, rings)
         for r in range(world):
             assert got[r][:want_rs[r].size].tobytes() == want_rs[r].tobytes(), (case, "rs", r, on_dev)
         got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, NP[dt]) for _ in xs],
-                  count, dt, op, 0, 4096, 4, on_dev)
+                  count, dt, op, 0, 4096, 4, on_dev, rings)
         for r in range(world):
             assert got[r].tobytes() == want_ar[r].tobytes(), (case, "ar", r, on_dev)
         # in place
         R = [to_dev(gpu, x) for x in xs] if on_dev else [x.copy() for x in xs]
         ps = (ctypes.c_void_p * world)(*[(ptr(r) if on_dev else r.ctypes.data) for r in R])
-        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, 0, 4096, 4) == 0, \
+        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, 0, 4096, 4, rings) == 0, \
             pgamd.last_error()
         for r in range(world):
             g = to_host(gpu, R[r]) if on_dev else R[r]
             assert g.tobytes() == want_ar[r].tobytes(), (case, "ar-inplace", r, on_dev)
         got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, [np.zeros(count * world, NP[dt]) for _ in xs],
-                  count, dt, 0, 0, 4096, 4, on_dev)
+                  count, dt, 0, 0, 4096, 4, on_dev, rings)
         for r in range(world):
             assert got[r].tobytes() == want_ag[r].tobytes(), (case, "ag", r, on_dev)
 
 
-def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch):
+@pytest.mark.parametrize("rings", [1, 2])
+def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch, rings):
     """Same inputs through the one-shot and through the W-1 round ring
     (PG_EAGER_ONESHOT=0): byte-identical outputs, doubles included."""
     world, count = 8, 509
@@ -311,7 +316,7 @@ def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch):
         for flag in ("1", "0"):
             monkeypatch.setenv("PG_EAGER_ONESHOT", flag)
             outs.append(sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, NP[dt]) for _ in xs],
-                            count, dt, op, 0, 4096, 4, True))
+                            count, dt, op, 0, 4096, 4, True, rings))
         for a, b in zip(*outs):
             assert a.tobytes() == b.tobytes(), (dt, op)
 
@@ -333,7 +338,7 @@ def test_all_gather_in_place(gpu, lib, oracle, world, count, eager):
                 recvs.append(buf)
             R = [to_dev(torch, b) for b in recvs] if on_dev else recvs
             rp = (ctypes.c_void_p * world)(*[(ptr(b) if on_dev else b.ctypes.data) for b in R])
-            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_GATHER, None, rp, count, dt, 0, 0, eager, 4) == 0, \
+            assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_GATHER, None, rp, count, dt, 0, 0, eager, 4, 2) == 0, \
                 pgamd.last_error()
             for r in range(world):
                 got = to_host(torch, R[r]) if on_dev else R[r]

@@ -7,6 +7,7 @@ bit-exact, NaN results included (measured: gfx950 produces the same default
 NaN 0xfff8000000000000 for inf-inf / 0*inf as x86 SSE and propagates NaN
 payloads the same way)."""
 import hashlib
+import itertools
 
 import numpy as np
 import pytest
@@ -226,15 +227,17 @@ def test_fold_blocks_and_gather(gpu, lib, oracle):
     order); pgk_gather copies every range, 16-B and 4-B aligned forms."""
     import ctypes
     torch = gpu
-    for world, count, dt, op in ((2, 1001, 1, 0), (3, 10, 0, 1), (8, 65541, 1, 1), (5, 4, 1, 0), (4, 4099, 0, 0)):
+    cases = ((2, 1001, 1, 0), (3, 10, 0, 1), (8, 65541, 1, 1), (5, 4, 1, 0), (4, 4099, 0, 0), (7, 7001, 1, 0))
+    for (world, count, dt, op), rings in itertools.product(cases, (1, 2)):
         xs = [oracle.fill(count, dt, op, 77 + r) for r in range(world)]
-        want = oracle.ring_all_reduce(xs, dt, op)[0]
+        want = oracle.ring_all_reduce(xs, dt, op, rings)[0]
         D = [to_dev(torch, x) for x in xs]
         out = torch.zeros(count, dtype=D[0].dtype, device="cuda")
         srcs = (ctypes.c_void_p * world)(*[ptr(d) for d in D])
         blk = -(-count // world)
-        assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, dt, op, stream(torch)) == 0
-        assert to_host(torch, out).tobytes() == want.tobytes(), (world, count, dt, op)
+        assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, rings, dt, op, stream(torch)) == 0
+        assert to_host(torch, out).tobytes() == want.tobytes(), (world, count, dt, op, rings)
+    assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, 3, 1, 0, stream(torch)) == -1
     # gather: ranges of different sizes/alignments into one buffer
     src = torch.arange(1 << 16, dtype=torch.int32, device="cuda")
     dst = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")

@@ -112,29 +112,33 @@ def test_splitmix_stream(oracle):
     assert np.array_equal(a.view(np.uint32), (z >> np.uint64(32)).astype(np.uint32))
 
 
-def test_ring_simulator_semantics(oracle):
+@pytest.mark.parametrize("rings", [1, 2])
+def test_ring_simulator_semantics(oracle, rings):
     """orc_ring_*: integer sums equal the wrapped total; doubles follow the
-    documented fold order x[b+1] op x[b+2] op ... op x[b]."""
+    documented fold order x[b+1] op x[b+2] op ... op x[b] (with two rings the
+    second part of each block, from ceil(len/2) on, x[b-1] op ... op x[b])."""
     rng = np.random.default_rng(7)
     for world in (1, 2, 3, 5, 8):
         for count in (0, 1, 7, 64, 1001):
             xs = [rng.integers(-2**31, 2**31, count, dtype=np.int64).astype(np.int32) for _ in range(world)]
-            outs = oracle.ring_reduce_scatter(xs, 0, 0)
+            outs = oracle.ring_reduce_scatter(xs, 0, 0, rings)
             total = np.zeros(count, np.uint32)
             for x in xs:
                 total += x.view(np.uint32)
             for b in range(world):
                 off, ln = oracle.ring_block(count, world, b)
                 assert np.array_equal(outs[b].view(np.uint32), total[off:off + ln])
-            fs = [rng.standard_normal(count) for _ in range(world)]
-            outs = oracle.ring_reduce_scatter(fs, 1, 0)
+            fs = [rng.standard_normal(count) * np.exp2(rng.integers(-30, 31, count)) for _ in range(world)]
+            outs = oracle.ring_reduce_scatter(fs, 1, 0, rings)
             for b in range(world):
                 off, ln = oracle.ring_block(count, world, b)
-                acc = fs[(b + 1) % world][off:off + ln].copy()
-                for j in range(2, world + 1):
-                    acc = acc + fs[(b + j) % world][off:off + ln]
-                assert acc.tobytes() == outs[b].tobytes()
-            ar = oracle.ring_all_reduce(fs, 1, 0)
+                h = ln if rings == 1 else (ln + 1) // 2
+                for lo, hi, step in ((0, h, 1), (h, ln, world - 1)):
+                    acc = fs[(b + step) % world][off + lo:off + hi].copy()
+                    for j in range(2, world + 1):
+                        acc = acc + fs[(b + j * step) % world][off + lo:off + hi]
+                    assert acc.tobytes() == outs[b][lo:hi].tobytes()
+            ar = oracle.ring_all_reduce(fs, 1, 0, rings)
             full = np.concatenate(outs) if outs else np.zeros(0)
             assert all(r.tobytes() == full.tobytes() for r in ar)
             ag = oracle.ring_all_gather(fs, 1)

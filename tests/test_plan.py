@@ -24,17 +24,28 @@ def test_block_range_matches_oracle(oracle):
 
 
 def test_plan_rejects_bad_arguments(lib):
-    assert lib.pg_plan_reduce_scatter(0, 0, 8, 0, 16, 0, 1, 0, None, 0) == -1
-    assert lib.pg_plan_reduce_scatter(2, 2, 8, 0, 16, 0, 1, 0, None, 0) == -1
-    assert lib.pg_plan_reduce_scatter(0, 2, -1, 0, 16, 0, 1, 0, None, 0) == -1
-    assert lib.pg_plan_reduce_scatter(0, 2, 8, 9, 16, 0, 1, 0, None, 0) == -1
-    assert lib.pg_plan_all_gather(0, 2, 8, 9, 1, None, 0) == -1
-    assert lib.pg_plan_reduce_scatter(0, 1, 8, 0, 16, 0, 1, 0, None, 0) == 0
+    assert lib.pg_plan_reduce_scatter(0, 0, 8, 0, 16, 0, 1, 2, 0, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(2, 2, 8, 0, 16, 0, 1, 2, 0, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(0, 2, -1, 0, 16, 0, 1, 2, 0, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(0, 2, 8, 9, 16, 0, 1, 2, 0, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(0, 2, 8, 0, 16, 0, 1, 3, 0, None, 0) == -1      # rings 1 or 2
+    assert lib.pg_plan_reduce_scatter(0, 2, 8, 0, 16, 0, 1, 0, 0, None, 0) == -1
+    assert lib.pg_plan_all_gather(0, 2, 8, 9, 1, 2, None, 0) == -1
+    assert lib.pg_plan_all_gather(0, 2, 8, 0, 1, 3, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(0, 1, 8, 0, 16, 0, 1, 2, 0, None, 0) == 0
+
+
+def test_block_parts():
+    for ln in (0, 1, 2, 7, 8, 1001):
+        assert pgamd.block_part(ln, 1, 0) == (0, ln)
+        h = (ln + 1) // 2
+        assert pgamd.block_part(ln, 2, 0) == (0, h)
+        assert pgamd.block_part(ln, 2, 1) == (h, ln - h)
 
 
 def test_plan_shape():
-    # W=4, count=4096 int32, 1 KiB segments, no eager: 3 rounds x 1 segment... block=1024 elems=4 KiB -> 4 segs
-    st = pgamd.plan_reduce_scatter(1, 4, 4096, 0, 1024, 0, 2)
+    # W=4, count=4096 int32, 1 KiB segments, no eager, one ring: block=1024 elems=4 KiB -> 4 segs
+    st = pgamd.plan_reduce_scatter(1, 4, 4096, 0, 1024, 0, 2, rings=1)
     assert [s["round"] for s in st] == [0] * 4 + [1] * 4 + [2] * 4
     assert [s["batch"] for s in st] == [0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5]
     assert all(s["send_wait"] == (s["round"] > 0) for s in st)
@@ -43,47 +54,94 @@ def test_plan_shape():
     # rank 1 ends with block 1: last round receives block (1-2-2) % 4 = 1
     assert all(s["red_src_off"] == 1024 * 4 + s["recv_off"] for s in last)
     # eager: a block <= eager_max bytes is one segment
-    st = pgamd.plan_reduce_scatter(0, 4, 4096, 0, 1024, 1 << 20, 4)
+    st = pgamd.plan_reduce_scatter(0, 4, 4096, 0, 1024, 1 << 20, 4, rings=1)
     assert len(st) == 3
 
 
+def test_plan_shape_two_rings():
+    # same shape, two rings: each 4 KiB block splits into two 2 KiB parts of 2 segments each;
+    # a batch carries 2 segment indices of each ring, clockwise first
+    st = pgamd.plan_reduce_scatter(1, 4, 4096, 0, 1024, 0, 2, rings=2)
+    assert len(st) == 3 * 4
+    assert [s["send_peer"] for s in st[:4]] == [1, 1, -1, -1]
+    assert all(s["recv_peer"] == -s["send_peer"] for s in st)
+    assert [s["batch"] for s in st] == [0] * 4 + [1] * 4 + [2] * 4
+    cw = [s for s in st if s["send_peer"] == 1]
+    ccw = [s for s in st if s["send_peer"] == -1]
+    # round 0: clockwise sends part 0 of block 0 (rank-1), counter-clockwise part 1 of block 2 (rank+1)
+    assert [s["send_off"] for s in cw if s["round"] == 0] == [0, 1024]
+    assert [s["send_off"] for s in ccw if s["round"] == 0] == [2 * 4096 + 2048, 2 * 4096 + 3072]
+    # ring 1 stages at ceil(B/2) elements into the staging block; events do not collide
+    assert all(s["recv_off"] >= 2048 for s in ccw if s["round"] == 0)
+    assert {s["seg"] for s in cw}.isdisjoint({s["seg"] for s in ccw})
+    # the last round lands both parts of block 1 in OUT: [0, 2 KiB) and [2 KiB, 4 KiB)
+    assert sorted(s["recv_off"] for s in st if s["round"] == 2) == [0, 1024, 2048, 3072]
+    assert all(s["recv_buf"] == pgamd.PG_BUF_OUT for s in st if s["round"] == 2)
+
+
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
-def test_plan_edges_pair_up(world):
+def test_plan_edges_pair_up(world, rings):
+    """Per directed edge, the sizes one rank sends equal, in order, the sizes its peer receives."""
     for count, dt, cb, eager, infl in itertools.product((0, 1, 9, 1000, 4099), (0, 1), (8, 100, 4096), (0, 4096), (1, 3)):
-        plans = [pgamd.plan_reduce_scatter(r, world, count, dt, cb, eager, infl) for r in range(world)]
+        plans = [pgamd.plan_reduce_scatter(r, world, count, dt, cb, eager, infl, rings=rings) for r in range(world)]
         for r in range(world):
-            sends = [s["send_bytes"] for s in plans[r] if s["send_bytes"]]
-            recvs = [s["recv_bytes"] for s in plans[(r + 1) % world] if s["recv_bytes"]]
-            assert sends == recvs, (world, r, count, dt, cb)
+            for q in range(world):
+                sends = [s["send_bytes"] for s in plans[r] if s["send_bytes"] and (r + s["send_peer"]) % world == q]
+                recvs = [s["recv_bytes"] for s in plans[q] if s["recv_bytes"] and (q + s["recv_peer"]) % world == r]
+                assert sends == recvs, (world, r, q, count, dt, cb)
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
-def test_plan_reduce_scatter_matches_oracle(oracle, world):
+def test_plan_reduce_scatter_matches_oracle(oracle, world, rings):
     for dt, op, count, cb, infl in itertools.product((0, 1), (0, 1), (0, 1, 5, 64, 1001), (8, 24, 4096), (1, 4)):
         xs = inputs(oracle, world, count, dt, op, count + world)
-        want = oracle.ring_reduce_scatter(xs, dt, op)
+        want = oracle.ring_reduce_scatter(xs, dt, op, rings)
         if world == 1:
             continue
-        got, _ = ring_reduce_scatter(xs, dt, op, cb, eager_max=0, inflight=infl)
+        got, _ = ring_reduce_scatter(xs, dt, op, cb, eager_max=0, inflight=infl, rings=rings)
         for r in range(world):
             assert got[r].tobytes() == want[r].tobytes(), (world, r, dt, op, count, cb)
 
 
+def test_two_rings_fold_order_differs_for_double(oracle):
+    """Rings change which neighbour is folded first in the second half of each
+    block: for doubles that is visible in the bits (so every transport must use
+    the same PG_RINGS), for int32 it is not (two's complement is associative)."""
+    # magnitudes spread over 2^-20 .. 2^20, so partial sums round (oracle.fill's
+    # U[-1,1) multiples of 2^-52 add exactly in either order up to the last step)
+    rng = np.random.default_rng(5)
+    xs = [rng.standard_normal(4000) * np.exp2(rng.integers(-20, 21, 4000)) for _ in range(4)]
+    a, b = oracle.ring_reduce_scatter(xs, 1, 0, 1), oracle.ring_reduce_scatter(xs, 1, 0, 2)
+    assert all(x[:len(x) // 2].tobytes() == y[:len(y) // 2].tobytes() for x, y in zip(a, b))
+    assert any(x.tobytes() != y.tobytes() for x, y in zip(a, b))
+    bound = 2 * 3 * 2.0**-53 * sum(np.abs(v) for v in xs)       # 2 * (W-1) u * sum|x|, element-wise
+    for blk, (x, y) in enumerate(zip(a, b)):
+        off = blk * 1000
+        assert np.all(np.abs(x - y) <= bound[off:off + 1000])
+    xi = inputs(oracle, 4, 4000, 0, 1, 6)
+    ai, bi = oracle.ring_reduce_scatter(xi, 0, 1, 1), oracle.ring_reduce_scatter(xi, 0, 1, 2)
+    assert all(x.tobytes() == y.tobytes() for x, y in zip(ai, bi))
+
+
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_plan_all_reduce_in_place_matches_oracle(oracle, world):
+def test_plan_all_reduce_in_place_matches_oracle(oracle, world, rings):
     for dt, op, count in itertools.product((0, 1), (0, 1), (1, 7, 100, 1001)):
         xs = inputs(oracle, world, count, dt, op, 99 + count)
-        want = oracle.ring_all_reduce(xs, dt, op)
-        got = ring_all_reduce(xs, dt, op, chunk_bytes=40, eager_max=0, inflight=2)
+        want = oracle.ring_all_reduce(xs, dt, op, rings)
+        got = ring_all_reduce(xs, dt, op, chunk_bytes=40, eager_max=0, inflight=2, rings=rings)
         for r in range(world):
             assert got[r].tobytes() == want[r].tobytes(), (world, r, dt, op, count)
 
 
+@pytest.mark.parametrize("rings", [1, 2])
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
-def test_plan_all_gather_matches_oracle(oracle, world):
+def test_plan_all_gather_matches_oracle(oracle, world, rings):
     for dt, count in itertools.product((0, 1), (0, 1, 13, 512)):
         xs = inputs(oracle, world, count, dt, 0, 7 + count)
         want = oracle.ring_all_gather(xs, dt)
-        got = ring_all_gather(xs, dt)
+        got = ring_all_gather(xs, dt, rings)
         for r in range(world):
             assert got[r].tobytes() == want[r].tobytes()

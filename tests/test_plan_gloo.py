@@ -6,6 +6,7 @@ real point-to-point messages between processes; the segment reduction is done
 test-side with numpy.  Results must equal the oracle's ring simulator bit for
 bit.  This pins the multi-process schedule: every send pairs with the right
 neighbour's receive, in order, with matching sizes."""
+import itertools
 import os
 import pathlib
 import socket
@@ -37,18 +38,18 @@ def _worker(rank, world, port, q):
         from oracle.pyoracle import Oracle
         from plan_sim import NP, np_reduce
         orc = Oracle()
-        right, left = (rank + 1) % world, (rank - 1) % world
         fails = []
-        for dt, op, count, cb, infl in ((0, 0, 1000, 64, 2), (1, 0, 4099, 256, 4), (1, 1, 77, 8, 1),
-                                        (0, 1, 3, 4, 1), (1, 0, 0, 64, 1)):
+        for (dt, op, count, cb, infl), rings in itertools.product(
+                ((0, 0, 1000, 64, 2), (1, 0, 4099, 256, 4), (1, 1, 77, 8, 1), (0, 1, 3, 4, 1), (1, 0, 0, 64, 1)),
+                (1, 2)):
             es = 4 if dt == 0 else 8
             xs = [orc.fill(count, dt, op, 500 + 17 * q_ + count) for q_ in range(world)]
-            want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+            want = orc.ring_reduce_scatter(xs, dt, op, rings)[rank]
             off, ln = pgamd.block_range(count, world, rank)
             bmax = -(-count // world) * es if count else 0
             bufs = {pgamd.PG_BUF_SRC: xs[rank].copy().view(np.uint8), pgamd.PG_BUF_OUT: np.zeros(ln * es, np.uint8),
                     pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)}
-            steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl)
+            steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl, rings=rings)
             i = 0
             while i < len(steps):
                 j = i
@@ -58,10 +59,10 @@ def _worker(rank, world, port, q):
                 for s in steps[i:j]:
                     if s["send_bytes"]:
                         t = torch.from_numpy(bufs[s["send_buf"]][s["send_off"]:s["send_off"] + s["send_bytes"]].copy())
-                        reqs.append(dist.isend(t, right))
+                        reqs.append(dist.isend(t, (rank + s["send_peer"]) % world))
                     if s["recv_bytes"]:
                         t = torch.empty(s["recv_bytes"], dtype=torch.uint8)
-                        reqs.append((dist.irecv(t, left), t, s))
+                        reqs.append((dist.irecv(t, (rank + s["recv_peer"]) % world), t, s))
                 for r_ in reqs:
                     if isinstance(r_, tuple):
                         r_[0].wait()
@@ -78,7 +79,7 @@ def _worker(rank, world, port, q):
                 i = j
             got = bufs[pgamd.PG_BUF_OUT].view(NP[dt])
             if got.tobytes() != want.tobytes():
-                fails.append((dt, op, count, cb))
+                fails.append((dt, op, count, cb, rings))
         q.put((rank, fails))
     finally:
         dist.destroy_process_group()
