@@ -514,7 +514,32 @@ def native_crosscheck(lib, h, rank, world, x_full, dt_full):
     return res
 
 
-def ring_leg(lib, args, rank, world, transport):
+def _one_ring(lib, rank, world, x, out, count, dt):
+    """The same timed reduce-scatter over one clockwise ring (PG_RINGS=1, a
+    second handle and RCCL communicator), to show what the counter-rotating
+    second ring buys on this node."""
+    saved = {k: os.environ.get(k) for k in ("PG_RINGS", "PG_PORT")}
+    os.environ["PG_RINGS"] = "1"
+    os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + 4)
+    h1 = ctypes.c_void_p()
+    try:
+        if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h1)) != 0:
+            return {"error": "connect_process_group: " + pgamd.last_error()}
+        wall = _timed_rs(lib, h1, x, out, count, dt, pgamd.OP_SUM, 3, world)
+        payload = count * pgamd.ELEM_SIZE[dt]
+        return {"ms_per_reduce_scatter": round(wall * 1e3, 3), "algbw_gibs": round(payload / wall / GIB, 2),
+                "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2)}
+    finally:
+        if h1.value:
+            lib.pg_close(h1)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def ring_leg(lib, args, rank, world, transport, sink):
     """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3-5.
     transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads).
     Rows of the sweeps follow the reference's CSV discipline (README.md:85):
@@ -538,6 +563,7 @@ def ring_leg(lib, args, rank, world, transport):
         hd = pgamd.head(h)
         res = {"workload": cfg, "transport": {"rccl": "RCCL P2P ring over xGMI",
                                               "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order"}[transport]}
+        sink[transport] = res          # visible to the watchdog's print while the leg runs
         x = _pattern(count, rank, world, dt, pgamd.OP_SUM)
         off, ln = pgamd.block_range(count, world, rank)
         out = torch.empty(max(ln, 1), dtype=x.dtype, device="cuda")
@@ -553,7 +579,14 @@ def ring_leg(lib, args, rank, world, transport):
                     "algbw_gibs": round(payload / wall / GIB, 2),
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
                     "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
-                    "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight)})
+                    "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
+                    "rings": int(os.environ.get("PG_RINGS", "2"))})
+        if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
+            progress(rank, f"  {transport}: one-ring comparison")
+            try:
+                res["one_ring"] = _one_ring(lib, rank, world, x, out, count, dt)
+            except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
+                res["one_ring"] = {"error": f"{type(e).__name__}: {e}"}
         if os.environ.get("PG_BENCH_ONE_GPU") == "1":
             res["rccl_native"] = "skipped: ranks share one GPU (RCCL refuses duplicate devices)"
         else:
@@ -712,8 +745,18 @@ def main():
 
         def _expire():
             if line is not None:
-                ring["watchdog"] = f"ring leg exceeded {args.ring_timeout} s; unfinished transports omitted"
-                print(json.dumps(line), flush=True)
+                ring["watchdog"] = (f"ring leg exceeded {args.ring_timeout} s; the leg that was running is "
+                                    "reported up to where it stopped, later ones are omitted")
+                txt = None
+                for _ in range(20):          # the main thread may be adding to the ring dict right now
+                    try:
+                        txt = json.dumps(line)
+                        break
+                    except (RuntimeError, ValueError):
+                        time.sleep(0.05)
+                if txt is None:
+                    txt = json.dumps({k: v for k, v in line.items() if k != "ring"})
+                print(txt, flush=True)
             os._exit(0)
 
         dog = threading.Timer(args.ring_timeout, _expire)
@@ -722,9 +765,9 @@ def main():
         for transport in args.transports.split(","):
             progress(rank, f"ring leg: {transport}")
             try:
-                ring[transport] = ring_leg(lib, args, rank, world, transport)
+                ring_leg(lib, args, rank, world, transport, ring)
             except Exception as e:  # the primary measurement stands on its own
-                ring[transport] = {"error": f"{type(e).__name__}: {e}"}
+                ring.setdefault(transport, {})["error"] = f"{type(e).__name__}: {e}"
             barrier(world)
         dog.cancel()
 
