@@ -35,9 +35,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, oneshot_max, zero_copy="1"):
+def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max), PG_XGMI_ZERO_COPY=zero_copy)
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max), PG_XGMI_ZERO_COPY=zero_copy,
+                      PG_RINGS=str(rings))
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -63,7 +64,7 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1"):
                 on_dev = rank % 2 == 0
             xs = [orc.fill(count, dt, op, 700 + 13 * i + r) for r in range(world)]
             if coll == "rs":
-                want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+                want = orc.ring_reduce_scatter(xs, dt, op, rings)[rank]
                 recv = np.zeros(max(want.size, 1), NP[dt])
             elif coll == "ag":
                 want = orc.ring_all_gather(xs, dt)[rank]
@@ -71,7 +72,7 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1"):
                 if in_place:
                     recv[rank * count:(rank + 1) * count] = xs[rank]
             else:
-                want = orc.ring_all_reduce(xs, dt, op)[rank]
+                want = orc.ring_all_reduce(xs, dt, op, rings)[rank]
                 recv = xs[rank].copy() if in_place else np.zeros(count, NP[dt])
             send = xs[rank] if xs[rank].size else np.zeros(1, NP[dt])
             if on_dev:
@@ -99,18 +100,21 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1"):
     q.put((rank, fails))
 
 
-@pytest.mark.parametrize("world,oneshot_max,zero_copy", [(2, 1 << 20, "1"), (3, 1 << 20, "1"), (4, 1 << 20, "1"),
-                                                         (8, 1 << 20, "1"), (2, 0, "1"), (5, 0, "1"),
-                                                         (4, 1 << 40, "1"), (3, 1 << 20, "0"), (4, 0, "0")])
-def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy):
+@pytest.mark.parametrize("world,oneshot_max,zero_copy,rings", [
+    (2, 1 << 20, "1", 2), (3, 1 << 20, "1", 2), (4, 1 << 20, "1", 2), (8, 1 << 20, "1", 2), (2, 0, "1", 2),
+    (5, 0, "1", 2), (4, 1 << 40, "1", 2), (3, 1 << 20, "0", 2), (4, 0, "0", 2), (4, 1 << 20, "1", 1),
+    (3, 1 << 40, "0", 1)])
+def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy, rings):
     """oneshot_max selects the all-reduce form: 0 = always reduce-scatter +
     gather, 2^40 = always the one-shot fold, 1 MiB = the default split.
-    zero_copy "0" forces the slot copy for every input."""
+    zero_copy "0" forces the slot copy for every input.  rings: PG_RINGS (the
+    fold order of each block's second half)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max, zero_copy)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max, zero_copy, rings))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = []

@@ -58,6 +58,10 @@ static const V kV[] = {
     {"oneshot 256x4 lds48 (3 WG/CU)", 0, 256, 4, 48, 0},
     {"oneshot 256x4 lds32 (5 WG/CU)", 0, 256, 4, 32, 0},
     {"oneshot 256x8 lds96 (1 WG/CU)", 0, 256, 8, 96, 0},
+    {"oneshot 256x2 lds0", 0, 256, 2, 0, 0},
+    {"oneshot 256x4 lds0", 0, 256, 4, 0, 0},
+    {"oneshot 256x8 lds0", 0, 256, 8, 0, 0},
+    {"oneshot 512x4 lds0", 0, 512, 4, 0, 0},
     {"persist 1024 x2/CU", 1, 1024, 1, 0, 2},
     {"persist 1024 x1/CU", 1, 1024, 1, 0, 1},
     {"persist 512 x4/CU", 1, 512, 1, 0, 4},
@@ -95,6 +99,7 @@ extern "C" int lab2_launch(int vi, double* d, const double* s, size_t n, void* s
       case 1024 * 16 + 2: go1<1024, 2>(v, vd, vs, nvec, st); break;
       case 512 * 16 + 2: go1<512, 2>(v, vd, vs, nvec, st); break;
       case 512 * 16 + 4: go1<512, 4>(v, vd, vs, nvec, st); break;
+      case 256 * 16 + 2: go1<256, 2>(v, vd, vs, nvec, st); break;
       case 256 * 16 + 4: go1<256, 4>(v, vd, vs, nvec, st); break;
       case 256 * 16 + 8: go1<256, 8>(v, vd, vs, nvec, st); break;
       default: return -5;

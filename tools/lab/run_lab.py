@@ -29,7 +29,7 @@ POOL = 2 << 30
 pd = torch.empty(POOL // 8, dtype=torch.float64, device="cuda").uniform_(-1, 1)
 ps = torch.empty(POOL // 8, dtype=torch.float64, device="cuda").uniform_(-1, 1)
 variants = [-1] + [v for v in range(64) if lab.lab_name(v)]
-for size in (1 << 28, 1 << 30):
+for size in tuple(int(a) << 20 for a in sys.argv[1:]) or (1 << 28, 1 << 30):
     n = size // 8
     nch = POOL // size
     times = {v: [] for v in variants}

@@ -37,7 +37,7 @@ for v in range(64):                      # keep the variants that launch (LDS re
             variants.append(v)
         else:
             print(f"skip {lab.lab2_name(v).decode()}: launch rc {rc}", flush=True)
-for size in (1 << 28, 1 << 30):
+for size in tuple(int(a) << 20 for a in sys.argv[1:]) or (1 << 28, 1 << 30):
     n = size // 8
     nch = POOL // size
     times = {v: [] for v in variants}
