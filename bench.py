@@ -539,6 +539,20 @@ def _one_ring(lib, rank, world, x, out, count, dt):
                 os.environ[k] = v
 
 
+def _link_probe(lib, h, rank, world, nbytes=256 << 20, reps=5):
+    """Copy rates of this node's xGMI links as the xgmi transport uses them
+    (pgx_xgmi_link_probe): one link pulled / pushed, all links pulled /
+    pushed at once; GB/s per rank, min / median / max over ranks."""
+    g = (ctypes.c_double * 4)()
+    if lib.pgx_xgmi_link_probe(h, nbytes, reps, g) != 0:
+        return {"error": pgamd.last_error()}
+    out = {"bytes": nbytes, "reps": reps, "unit": "GB/s per rank (1e9 B/s moved by the rank)"}
+    for i, name in enumerate(("read_one_link", "write_one_link", "read_all_links", "write_all_links")):
+        per = gather_over_ranks(g[i], rank, world)
+        out[name] = {"min": round(min(per), 1), "median": round(float(np.median(per)), 1), "max": round(max(per), 1)}
+    return out
+
+
 def ring_leg(lib, args, rank, world, transport, sink):
     """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3-5.
     transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads).
@@ -581,6 +595,9 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
                     "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
                     "rings": int(os.environ.get("PG_RINGS", "2"))})
+        if transport == "xgmi":          # (one-GPU rehearsal: every "link" is the same device)
+            progress(rank, f"  {transport}: link probe")
+            res["link_probe"] = _link_probe(lib, h, rank, world)
         if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
             progress(rank, f"  {transport}: one-ring comparison")
             try:

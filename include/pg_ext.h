@@ -148,6 +148,13 @@ PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
  * unique id and the xgmi IPC handles. */
 PG_API int pgx_boot_selftest(const char *serverlist, int rank, int port, int value, int *out);
 
+/* xgmi transport only, collective: the copy rates this node's links give
+ * (pgk_gather launches, HIP events, `reps` launches of `bytes` per phase).
+ * gbs[0] read one link (peer rank+1 -> me), gbs[1] write one link (me -> rank+1),
+ * gbs[2] read from all peers at once, gbs[3] write to all peers at once;
+ * 1e9 bytes/s moved by this rank.  bytes: a multiple of 4 KiB. */
+PG_API int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs);
+
 /* Last error message of the calling thread ("" if none). */
 PG_API const char *pg_last_error(void);
 

@@ -526,3 +526,65 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
   return 0;
 }
+
+/* ---- link probe ----------------------------------------------------------------
+ * Measures what the transport's traffic rides on ("measure
+ * the unidirectional per-link rate with a P2P probe before quoting roofline for
+ * the ring").  Every rank runs the same four phases, each `reps` copy launches
+ * of `bytes` (pgk_gather) timed with HIP events, with barriers in between:
+ *   0 read one:  peer (r+1)'s X0  -> my X1              (one link, pulled)
+ *   1 write one: my X0            -> peer (r+1)'s X1     (one link, pushed)
+ *   2 read all:  bytes/(W-1) from every peer's X0 -> my X1   (all links, pulled)
+ *   3 write all: bytes/(W-1) of my X0 -> every peer's X1, at my own offset
+ * gbs[phase] = bytes * reps / time on this rank (1e9 B/s).  Collective. */
+int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
+  struct pg *pg = (struct pg *)pg_handle;
+  if (!pg || !pg->impl || pg->transport != PG_TRANSPORT_XGMI || pg->world_size < 2 || !gbs || reps < 1 ||
+      bytes < 4096 || (bytes & 4095)) {
+    pg_set_error("pgx_xgmi_link_probe: needs an xgmi handle with world >= 2, bytes a multiple of 4 KiB, reps >= 1");
+    return -1;
+  }
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  const int W = pg->world_size, r = pg->rank, right = (r + 1) % W;
+  if (ensure(pg, XG_REG_X, bytes)) return -1;
+  PG_CHECK_HIP(hipMemsetAsync(slot(x, XG_REG_X, r, 0), r + 1, bytes, im->red));
+  PG_CHECK_HIP(hipStreamSynchronize(im->red));
+  size_t part = (bytes / (size_t)(W - 1)) & ~(size_t)15;
+  hipEvent_t e0, e1;
+  PG_CHECK_HIP(hipEventCreate(&e0));
+  PG_CHECK_HIP(hipEventCreate(&e1));
+  int rc = 0;
+  for (int phase = 0; phase < 4 && rc == 0; ++phase) {
+    void *dst[16];
+    const void *src[16];
+    size_t nb[16];
+    int k = 0;
+    if (phase == 0) { dst[0] = slot(x, XG_REG_X, r, 1); src[0] = slot(x, XG_REG_X, right, 0); nb[0] = bytes; k = 1; }
+    if (phase == 1) { dst[0] = slot(x, XG_REG_X, right, 1); src[0] = slot(x, XG_REG_X, r, 0); nb[0] = bytes; k = 1; }
+    for (int q = 0; phase >= 2 && q < W; ++q) {
+      if (q == r) continue;
+      int my_idx = r < q ? r : r - 1;           /* my position among q's peers */
+      int q_idx = q < r ? q : q - 1;            /* q's position among mine     */
+      if (phase == 2) { dst[k] = slot(x, XG_REG_X, r, 1) + (size_t)q_idx * part; src[k] = slot(x, XG_REG_X, q, 0); }
+      else { dst[k] = slot(x, XG_REG_X, q, 1) + (size_t)my_idx * part; src[k] = slot(x, XG_REG_X, r, 0); }
+      nb[k++] = part;
+    }
+    if (barrier(pg)) { rc = -1; break; }
+    if (pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
+    if (rc == 0 && (hipEventRecord(e0, im->red) != hipSuccess)) rc = -1;
+    for (int i = 0; rc == 0 && i < reps; ++i)
+      if (pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
+    float ms = 0.f;
+    if (rc == 0 && (hipEventRecord(e1, im->red) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                    hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+      rc = -1;
+    size_t moved = phase < 2 ? bytes : part * (size_t)(W - 1);
+    gbs[phase] = rc == 0 && ms > 0.f ? (double)moved * reps / (ms * 1e-3) / 1e9 : 0.0;
+    if (barrier(pg)) rc = -1;                  /* nobody overwrites a slot a peer still reads */
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (rc && !pg_last_error()[0]) pg_set_error("xgmi probe: HIP event failure");
+  return rc;
+}

@@ -258,3 +258,54 @@ def test_xgmi_ipc_bit31_sizes(gpu):
                 p.kill()
     for rank, fails in results:
         assert not fails, (rank, fails)
+
+
+def _probe_worker(rank, world, port, q):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="60000")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    out = {}
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        g = (ctypes.c_double * 4)()
+        out["rc"] = lib.pgx_xgmi_link_probe(h, 64 << 20, 3, g)
+        out["gbs"] = list(g)
+        out["bad_rc"] = lib.pgx_xgmi_link_probe(h, 1000, 3, g)          # not a multiple of 4 KiB
+        lib.pg_close(h)
+    except Exception as e:
+        out["exception"] = repr(e)
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_link_probe(gpu, world):
+    """pgx_xgmi_link_probe: the four copy phases run collectively and report
+    positive rates (on the one-GPU box every "link" is the same device)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_probe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=150))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, out in results:
+        assert "exception" not in out, out
+        assert out["rc"] == 0 and all(v > 0 for v in out["gbs"]), (rank, out)
+        assert out["bad_rc"] == -1
