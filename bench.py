@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
-    ap.add_argument("--transports", default="rccl,xgmi",
-                    help="ring-leg transports, comma separated (rccl first: the north-star P2P ring)")
+    ap.add_argument("--transports", default="rccl,xgmi,xgmi_push",
+                    help="ring-leg transports, comma separated (rccl first: the north-star P2P ring; "
+                         "xgmi_push = PG_TRANSPORT=xgmi with PG_XGMI_MODE=push, timed call only)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
@@ -567,16 +568,21 @@ def ring_leg(lib, args, rank, world, transport, sink):
     es = pgamd.ELEM_SIZE[dt]
     hosts = " ".join(["127.0.0.1"] * world).encode()
     os.environ["PG_RANK"] = str(rank)
-    os.environ["PG_TRANSPORT"] = transport
-    os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + (17 if transport == "rccl" else 19))
+    os.environ["PG_TRANSPORT"] = "xgmi" if transport.startswith("xgmi") else transport
+    os.environ["PG_XGMI_MODE"] = "push" if transport == "xgmi_push" else "read"
+    os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) +
+                                {"rccl": 17, "xgmi": 19, "xgmi_push": 21}[transport])
+    core_only = transport == "xgmi_push"       # the correctness probe and the timed call
     h = ctypes.c_void_p()
     progress(rank, f"  {transport}: connect_process_group")
     if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
         raise RuntimeError("connect_process_group: " + pgamd.last_error())
     try:
         hd = pgamd.head(h)
-        res = {"workload": cfg, "transport": {"rccl": "RCCL P2P ring over xGMI",
-                                              "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order"}[transport]}
+        res = {"workload": cfg, "transport": {
+            "rccl": "RCCL P2P ring over xGMI",
+            "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order",
+            "xgmi_push": "each block written to its owner over xGMI (HIP IPC), folded locally in ring order"}[transport]}
         sink[transport] = res          # visible to the watchdog's print while the leg runs
         x = _pattern(count, rank, world, dt, pgamd.OP_SUM)
         off, ln = pgamd.block_range(count, world, rank)
@@ -595,6 +601,8 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
                     "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
                     "rings": int(os.environ.get("PG_RINGS", "2"))})
+        if core_only:
+            return res
         if transport == "xgmi":          # (one-GPU rehearsal: every "link" is the same device)
             progress(rank, f"  {transport}: link probe")
             res["link_probe"] = _link_probe(lib, h, rank, world)

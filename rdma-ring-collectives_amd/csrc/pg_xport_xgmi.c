@@ -53,6 +53,7 @@ struct xgmi_ctx {
   size_t oneshot_max;           /* all-reduce at most this many bytes: one-shot */
   void *bar;                    /* node-local shm barrier (pg_boot.c), or NULL */
   int zc;                       /* zero-copy inputs allowed (PG_XGMI_ZERO_COPY) */
+  int push;                     /* PG_XGMI_MODE=push: reduce-scatter writes, not reads */
   hipIpcMemHandle_t exp_h;      /* last export of a caller allocation       */
   unsigned long long exp_bid;
   void *exp_base;
@@ -184,6 +185,12 @@ int pg_xport_xgmi_init(struct pg *pg) {
   if (e && *e) x->oneshot_max = (size_t)strtoull(e, NULL, 0);
   e = getenv("PG_XGMI_ZERO_COPY");
   x->zc = !(e && *e == '0');
+  e = getenv("PG_XGMI_MODE");
+  if (e && *e && strcmp(e, "read") != 0 && strcmp(e, "push") != 0) {
+    pg_set_error("PG_XGMI_MODE=%s: expected read or push", e);
+    return -1;
+  }
+  x->push = e && strcmp(e, "push") == 0;
   x->imp = (struct xg_import *)calloc((size_t)pg->world_size * XG_IMPORTS, sizeof(struct xg_import));
   if (!x->imp) { pg_set_error("xgmi: out of host memory"); return -1; }
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
@@ -413,21 +420,96 @@ static int overlaps(const void *a, size_t na, const void *b, size_t nb) {
   return na && nb && x < y + nb && y < x + na;
 }
 
+/* ---- push mode (PG_XGMI_MODE=push) --------------------------------------------
+ * The same reduce-scatter with the xGMI traffic as writes instead of reads:
+ * every rank writes block q of its input into rank q's X[parity] at piece
+ * position r (one pgk_gather launch, all links at once), meets the others at
+ * a barrier, and folds its own block from local memory in ring order.  Local
+ * HBM traffic grows (W pieces read instead of one); which of the two is
+ * faster depends on whether the links move pushed or pulled bytes faster,
+ * which is what the link probe measures (pgx_xgmi_link_probe).  The choice
+ * is collective: every rank flags whether it can push (device input, 4-byte
+ * aligned, output not overlapping the input), and if any cannot, all of them
+ * take the read path.  pieces[q] = block `rank` of rank q's contribution. */
+static size_t push_stride(int count, int world, size_t es) {
+  size_t b = ((size_t)count + (size_t)world - 1) / (size_t)world;
+  return ((b ? b : 1) * es + 255) & ~(size_t)255;
+}
+
+static int push_inputs(struct pg *pg, const char *in, int count, int dt, int can, const char **pieces,
+                       int *pushed) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
+  const int W = pg->world_size, r = pg->rank, which = (int)(x->gen & 1);
+  const size_t es = pg_elem_size(dt), stride = push_stride(count, W, es);
+  *pushed = 0;
+  double t0 = us_now();
+  if (can) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  double t1 = us_now();
+  im->stats.sync_us += t1 - t0;
+  struct xg_desc mine;
+  memset(&mine, 0, sizeof(mine));
+  mine.ok = can && ((uintptr_t)in & 3) == 0;
+  descs(x)[r] = mine;
+  if (barrier(pg)) return -1;
+  int all_ok = 1;
+  for (int q = 0; q < W; ++q) all_ok &= descs(x)[q].ok;
+  im->stats.barrier_us += us_now() - t1;
+  if (!all_ok) {
+    /* everybody takes the read path, whose first step rewrites the descriptor
+     * page: meet once more so that no rank does so before all have read it */
+    return barrier(pg) ? -1 : 0;
+  }
+  if (ensure(pg, XG_REG_X, stride * (size_t)W)) return -1;
+  void *dst[16];
+  const void *src[16];
+  size_t nb[16];
+  int k = 0;
+  for (int q = 0; q < W; ++q) {
+    size_t qo, ql;
+    pg_block_range(count, W, q, &qo, &ql);
+    if (q == r) { pieces[q] = in + qo * es; continue; }
+    pieces[q] = slot(x, XG_REG_X, r, which) + (size_t)q * stride;
+    if (!ql) continue;
+    dst[k] = slot(x, XG_REG_X, q, which) + (size_t)r * stride;
+    src[k] = in + qo * es;
+    nb[k++] = ql * es;
+  }
+  double t2 = us_now();
+  pg_trace(pg, "xgmi push: %d pieces", k);
+  if (k && pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi: %s", pgk_last_error()); return -1; }
+  if (pg_stream_wait(im->red)) return -1;
+  double t3 = us_now();
+  im->stats.copy_us += t3 - t2;
+  im->stats.bytes_sent += (int64_t)((size_t)count * es);
+  if (barrier(pg)) return -1;                                /* every piece has landed */
+  im->stats.barrier_us += us_now() - t3;
+  *pushed = 1;
+  return 0;
+}
+
 int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
+  struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
-  int rd = is_dev(recvbuf), zc, fail;
+  int rd = is_dev(recvbuf), zc = 0, fail = 0, pushed = 0;
   const char *by_rank[16];
-  if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, len * es), by_rank,
-                   &zc, &fail))
+  size_t fold_off = off;
+  if (x->push && bytes) {
+    int can = is_dev(sendbuf) && !overlaps(sendbuf, bytes, recvbuf, len * es);
+    if (push_inputs(pg, (const char *)sendbuf, count, dt, can, by_rank, &pushed)) return -1;
+    if (pushed) fold_off = 0;                   /* by_rank[q] point at block `rank` itself */
+  }
+  if (!pushed && share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, len * es),
+                              by_rank, &zc, &fail))
     return -1;
   void *out = recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, len * es)) return -1;
     out = im->dout;
   }
-  if (!fail && fold_block(pg, out, by_rank, off, len, dt, op)) fail = 1;
+  if (!fail && fold_block(pg, out, by_rank, fold_off, len, dt, op)) fail = 1;
   if (finish(pg, zc, fail)) return -1;
   if (!rd && len && pg_copy_parallel(recvbuf, out, len * es)) return -1;
   return 0;
@@ -486,10 +568,16 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
   pg_block_range(count, pg->world_size, pg->rank, &off, &len);
-  int rd = is_dev(recvbuf), which = (int)(x->gen & 1), zc, fail;
+  int rd = is_dev(recvbuf), which = (int)(x->gen & 1), zc = 0, fail = 0, pushed = 0;
   const char *by_rank[16];
-  if (share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, bytes), by_rank, &zc,
-                   &fail))
+  size_t fold_off = off;
+  if (x->push && bytes > x->oneshot_max) {      /* same branch on every rank: same count */
+    int can = is_dev(sendbuf) && !overlaps(sendbuf, bytes, recvbuf, bytes);
+    if (push_inputs(pg, (const char *)sendbuf, count, dt, can, by_rank, &pushed)) return -1;
+    if (pushed) fold_off = 0;
+  }
+  if (!pushed && share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, bytes), by_rank,
+                              &zc, &fail))
     return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
@@ -514,7 +602,8 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
   } else {
     /* my block of the result goes to R[which] so that every rank can gather it */
     if (ensure(pg, XG_REG_R, bytes)) return -1;
-    if (!fail && fold_block(pg, slot(x, XG_REG_R, pg->rank, which) + off * es, by_rank, off, len, dt, op)) fail = 1;
+    if (!fail && fold_block(pg, slot(x, XG_REG_R, pg->rank, which) + off * es, by_rank, fold_off, len, dt, op))
+      fail = 1;
     double tb = us_now();
     if (barrier(pg)) return -1;
     im->stats.barrier_us += us_now() - tb;

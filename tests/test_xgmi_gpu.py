@@ -35,10 +35,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2):
+def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2, mode="read"):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
                       PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max), PG_XGMI_ZERO_COPY=zero_copy,
-                      PG_RINGS=str(rings))
+                      PG_RINGS=str(rings), PG_XGMI_MODE=mode, PG_BARRIER_TIMEOUT_MS="60000")
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -100,20 +100,24 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2):
     q.put((rank, fails))
 
 
-@pytest.mark.parametrize("world,oneshot_max,zero_copy,rings", [
-    (2, 1 << 20, "1", 2), (3, 1 << 20, "1", 2), (4, 1 << 20, "1", 2), (8, 1 << 20, "1", 2), (2, 0, "1", 2),
-    (5, 0, "1", 2), (4, 1 << 40, "1", 2), (3, 1 << 20, "0", 2), (4, 0, "0", 2), (4, 1 << 20, "1", 1),
-    (3, 1 << 40, "0", 1)])
-def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy, rings):
+@pytest.mark.parametrize("world,oneshot_max,zero_copy,rings,mode", [
+    (2, 1 << 20, "1", 2, "read"), (3, 1 << 20, "1", 2, "read"), (4, 1 << 20, "1", 2, "read"),
+    (8, 1 << 20, "1", 2, "read"), (2, 0, "1", 2, "read"), (5, 0, "1", 2, "read"), (4, 1 << 40, "1", 2, "read"),
+    (3, 1 << 20, "0", 2, "read"), (4, 0, "0", 2, "read"), (4, 1 << 20, "1", 1, "read"), (3, 1 << 40, "0", 1, "read"),
+    (2, 1 << 20, "1", 2, "push"), (4, 0, "1", 2, "push"), (8, 1 << 20, "1", 2, "push"), (3, 0, "1", 1, "push"),
+    (5, 0, "0", 2, "push")])
+def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy, rings, mode):
     """oneshot_max selects the all-reduce form: 0 = always reduce-scatter +
     gather, 2^40 = always the one-shot fold, 1 MiB = the default split.
     zero_copy "0" forces the slot copy for every input.  rings: PG_RINGS (the
-    fold order of each block's second half)."""
+    fold order of each block's second half).  mode: PG_XGMI_MODE (push: the
+    reduce-scatter writes each block to its owner; host, mixed and in-place
+    cases fall back to the read path on every rank together)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max, zero_copy, rings))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, oneshot_max, zero_copy, rings, mode))
              for r in range(world)]
     for p in procs:
         p.start()
