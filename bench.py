@@ -521,7 +521,7 @@ def _one_ring(lib, rank, world, x, out, count, dt):
     second ring buys on this node."""
     saved = {k: os.environ.get(k) for k in ("PG_RINGS", "PG_PORT")}
     os.environ["PG_RINGS"] = "1"
-    os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + 4)
+    os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + 6)    # MASTER_PORT + 23: no other leg uses it
     h1 = ctypes.c_void_p()
     try:
         if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h1)) != 0:
