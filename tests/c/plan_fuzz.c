@@ -1,0 +1,47 @@
+/* tests/c/plan_fuzz.c -- the ring planner (csrc/pg_plan.c, pure C) under
+ * AddressSanitizer + UndefinedBehaviorSanitizer: every shape in the grid below
+ * is planned for every rank, in one and two rings, reduce-scatter (plain and
+ * in place) and all-gather, and every offset a step names must lie inside the
+ * buffer it names.  Built and run by tests/test_plan_sanitize.py.  Exit 0 = ok. */
+#include <stdio.h>
+#include <stdlib.h>
+#include "pg.h"
+#include "pg_ext.h"
+int main(void) {
+  long total = 0;
+  int counts[] = {0, 1, 2, 3, 5, 7, 8, 9, 63, 64, 65, 1000, 1001, 4099, 20011};
+  size_t cbs[] = {4, 12, 100, 4096, 1 << 20};
+  for (int W = 1; W <= 9; ++W)
+    for (int ci = 0; ci < 15; ++ci)
+      for (int dt = 0; dt < 2; ++dt)
+        for (int cbi = 0; cbi < 5; ++cbi)
+          for (int eager = 0; eager <= 4096; eager += 4096)
+            for (int infl = 1; infl <= 3; ++infl)
+              for (int rings = 1; rings <= 2; ++rings)
+                for (int alias = 0; alias < 2; ++alias)
+                  for (int r = 0; r < W; ++r) {
+                    int n = pg_plan_reduce_scatter(r, W, counts[ci], dt, cbs[cbi], eager, infl, rings, alias, NULL, 0);
+                    if (n < 0) { printf("fail %d %d\n", W, r); return 1; }
+                    struct pg_step *st = malloc(sizeof(*st) * (n ? n : 1));
+                    int m = pg_plan_reduce_scatter(r, W, counts[ci], dt, cbs[cbi], eager, infl, rings, alias, st, n);
+                    if (m != n) return 2;
+                    /* the plan must name only in-range offsets */
+                    size_t es = dt ? 8 : 4, blk = ((size_t)counts[ci] + W - 1) / W;
+                    for (int i = 0; i < n; ++i) {
+                      if (st[i].send_buf == PG_BUF_SRC && (size_t)(st[i].send_off + st[i].send_bytes) > counts[ci] * es) return 3;
+                      if ((st[i].send_buf == PG_BUF_STAGE0 || st[i].send_buf == PG_BUF_STAGE1) &&
+                          (size_t)(st[i].send_off + st[i].send_bytes) > blk * es) return 4;
+                      if ((st[i].recv_buf == PG_BUF_STAGE0 || st[i].recv_buf == PG_BUF_STAGE1) &&
+                          (size_t)(st[i].recv_off + st[i].recv_bytes) > blk * es) return 5;
+                      if (st[i].recv_buf == PG_BUF_OUT && (size_t)(st[i].recv_off + st[i].recv_bytes) > blk * es) return 6;
+                    }
+                    total += n;
+                    free(st);
+                    n = pg_plan_all_gather(r, W, counts[ci], dt, alias, rings, NULL, 0);
+                    st = malloc(sizeof(*st) * (n ? n : 1));
+                    pg_plan_all_gather(r, W, counts[ci], dt, alias, rings, st, n);
+                    free(st);
+                  }
+  printf("ok %ld steps\n", total);
+  return 0;
+}
