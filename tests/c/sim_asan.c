@@ -1,0 +1,99 @@
+/* tests/c/sim_asan.c -- the host side of the ring path (plan, executor,
+ * staging hooks, eager one-shot, threads transport, pgx_reduce_host) under
+ * AddressSanitizer + UndefinedBehaviorSanitizer, on the GPU.  The library's
+ * host C files are compiled with the sanitizers into this executable (the
+ * gfx950 kernels are built as usual), so no preloading is involved.  Every
+ * result is compared bit for bit with the oracle's ring simulator
+ * (oracle/pg_oracle.c, linked in as the checker).  Built and run by
+ * tests/test_sanitize_gpu.py.  Exit 0 = every case matched. */
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "pg.h"
+#include "pg_ext.h"
+#include "../../oracle/pg_oracle.h"
+
+static int run_case(int world, int coll, int count, int dt, int op, size_t cb, size_t eager, int infl, int rings,
+                    int on_dev) {
+  size_t es = dt ? 8 : 4;
+  size_t rlen = coll == PG_COLL_ALL_GATHER ? (size_t)count * world : (size_t)count;
+  void *hs[16], *hr[16], *want[16], *ds[16], *dr[16], *sp[16], *rp[16], *outs[16];
+  for (int r = 0; r < world; ++r) {
+    hs[r] = malloc(count * es + 16);
+    hr[r] = calloc(rlen + 4, es);
+    want[r] = calloc(rlen + 4, es);
+    orc_fill(hs[r], (size_t)count, dt, op, 9000 + 31 * r + count);
+    if (on_dev) {
+      if (hipMalloc(&ds[r], count * es + 16) != hipSuccess || hipMalloc(&dr[r], (rlen + 4) * es) != hipSuccess) return -10;
+      hipMemcpy(ds[r], hs[r], count * es, hipMemcpyHostToDevice);
+      hipMemset(dr[r], 0, (rlen + 4) * es);
+    }
+    sp[r] = on_dev ? ds[r] : hs[r];
+    rp[r] = on_dev ? dr[r] : hr[r];
+  }
+  int rc;
+  if (coll == PG_COLL_REDUCE_SCATTER) {
+    for (int r = 0; r < world; ++r) outs[r] = want[r];
+    rc = orc_ring_reduce_scatter(world, hs, outs, count, dt, op, rings);
+  } else if (coll == PG_COLL_ALL_REDUCE) {
+    rc = orc_ring_all_reduce(world, hs, want, count, dt, op, rings);
+  } else {
+    rc = orc_ring_all_gather(world, hs, want, count, dt);
+  }
+  if (rc) return -11;
+  rc = pgx_sim_run(world, coll, sp, rp, count, dt, op, cb, eager, infl, rings);
+  if (rc) { fprintf(stderr, "pgx_sim_run: %s\n", pg_last_error()); return -12; }
+  int bad = 0;
+  for (int r = 0; r < world; ++r) {
+    size_t n = rlen;
+    if (coll == PG_COLL_REDUCE_SCATTER) {
+      size_t be = ((size_t)count + world - 1) / world, first = (size_t)r * be;
+      n = first >= (size_t)count ? 0 : (first + be > (size_t)count ? count - first : be);
+    }
+    if (on_dev) hipMemcpy(hr[r], dr[r], n * es ? n * es : 1, hipMemcpyDeviceToHost);
+    if (memcmp(hr[r], want[r], n * es)) bad = 1;
+    free(hs[r]); free(hr[r]); free(want[r]);
+    if (on_dev) { hipFree(ds[r]); hipFree(dr[r]); }
+  }
+  return bad;
+}
+
+int main(void) {
+  int fails = 0, cases = 0;
+  const int shapes[][6] = {  /* world, count, dt, op, chunk_bytes, inflight */
+      {2, 1001, 1, 0, 256, 2}, {3, 4099, 0, 1, 1024, 1}, {4, 100003, 1, 0, 1 << 16, 4}, {5, 7, 1, 1, 8, 3},
+      {8, 65541, 1, 0, 1 << 14, 4}, {8, 3, 0, 0, 64, 1}, {6, 2, 1, 1, 8, 2}, {4, 512, 1, 0, 4096, 4}};
+  for (size_t i = 0; i < sizeof(shapes) / sizeof(shapes[0]); ++i)
+    for (int coll = 0; coll < 3; ++coll)
+      for (int rings = 1; rings <= 2; ++rings)
+        for (int on_dev = 0; on_dev < 2; ++on_dev)
+          for (int eager = 0; eager <= 4096; eager += 4096) {
+            const int *s = shapes[i];
+            int rc = run_case(s[0], coll, s[1], s[2], s[3], (size_t)s[4], (size_t)eager, s[5], rings, on_dev);
+            ++cases;
+            if (rc) {
+              fprintf(stderr, "case W=%d count=%d dt=%d op=%d coll=%d rings=%d dev=%d eager=%d: %d\n", s[0], s[1],
+                      s[2], s[3], coll, rings, on_dev, eager, rc);
+              ++fails;
+            }
+          }
+  /* the host-operand reduce */
+  size_t n = (5u << 20) + 7;
+  double *d = malloc(n * 8), *s = malloc(n * 8), *w = malloc(n * 8);
+  orc_fill(d, n, 1, 0, 1);
+  orc_fill(s, n, 1, 0, 2);
+  memcpy(w, d, n * 8);
+  orc_reduce_inplace(w, s, n, 1, 0);
+  if (pgx_reduce_host(d, s, n, 1, 0, 1 << 20) || memcmp(d, w, n * 8)) { fprintf(stderr, "pgx_reduce_host\n"); ++fails; }
+  free(d); free(s); free(w);
+  printf("%s %d cases\n", fails ? "FAIL" : "ok", cases);
+  fflush(stdout);
+  fflush(stderr);
+  /* skip library finalizers: at unload the HIP runtime frees into ASan's
+   * AMDGPU device-allocator hook after it has been torn down, which trips an
+   * ASan CHECK unrelated to this code (observed on ROCm 7.2) */
+  _exit(fails ? 1 : 0);
+}
