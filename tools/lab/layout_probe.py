@@ -24,7 +24,13 @@ sep_s = [torch.empty(N, dtype=torch.float64, device="cuda").uniform_(-1, 1) for 
 pool = torch.empty(8 * N, dtype=torch.float64, device="cuda").uniform_(-1, 1)     # d0 s0 d1 s1 ...
 dpool = torch.empty(4 * N, dtype=torch.float64, device="cuda").uniform_(-1, 1)
 spool = torch.empty(4 * N, dtype=torch.float64, device="cuda").uniform_(-1, 1)
+g = torch.Generator(device="cuda").manual_seed(1234)
+bench_d = [torch.rand(N, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(4)]
+bench_s = [torch.rand(N, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(4)]
+pool8 = torch.empty(16 * N, dtype=torch.float64, device="cuda").uniform_(-1, 1)           # size-table layout
 layouts = {
+    "bench.py tensors (rand*2-1)": lambda i: (bench_d[i].data_ptr(), bench_s[i].data_ptr()),
+    "4 GiB pool, 8 pairs": lambda i: (pool8.data_ptr() + 2 * (2 * i) * B, pool8.data_ptr() + (4 * i + 1) * B),
     "separate tensors (bench)": lambda i: (sep_d[i].data_ptr(), sep_s[i].data_ptr()),
     "one pool, d/s interleaved": lambda i: (pool.data_ptr() + 2 * i * B, pool.data_ptr() + (2 * i + 1) * B),
     "one pool per operand": lambda i: (dpool.data_ptr() + i * B, spool.data_ptr() + i * B),
