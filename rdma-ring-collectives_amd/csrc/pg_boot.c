@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <sys/types.h>
 #include <time.h>
 #include <unistd.h>
@@ -142,9 +143,18 @@ static int io_full(int fd, void *buf, size_t n, int writing) {
  * all-gather, barriers).  Retry/backoff and the 0xA5 ready token follow the
  * reference's bootstrap (src/pg_net.c:298-436, :699-710). */
 
-static int tcp_nodelay(int fd) {
-  int one = 1;
-  return setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+/* Established star connections: no Nagle delay, and every send/recv bounded by
+ * PG_BARRIER_TIMEOUT_MS (default 300 s), so a dead peer turns an all-gather or
+ * barrier into an error instead of a hang. */
+static void tune_socket(int fd) {
+  int one = 1, timeout_ms = 300000;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  env_int("PG_BARRIER_TIMEOUT_MS", &timeout_ms);
+  if (timeout_ms > 0) {
+    struct timeval tv = {timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  }
 }
 
 int pg_boot_open(struct pg *pg, int **fds_out) {
@@ -193,7 +203,7 @@ int pg_boot_open(struct pg *pg, int **fds_out) {
       uint8_t ack = 0xA5;
       if (io_full(c, &peer, sizeof(peer), 0) == 0 && peer > 0 && peer < W && fds[peer] < 0 &&
           io_full(c, &ack, 1, 1) == 0) {
-        tcp_nodelay(c);
+        tune_socket(c);
         fds[peer] = c;
         ++joined;
       } else {
@@ -223,7 +233,7 @@ int pg_boot_open(struct pg *pg, int **fds_out) {
       int32_t me = pg->rank;
       uint8_t ack = 0;
       if (io_full(fd, &me, sizeof(me), 1) == 0 && io_full(fd, &ack, 1, 0) == 0 && ack == 0xA5) {
-        tcp_nodelay(fd);
+        tune_socket(fd);
         fds[0] = fd;
         break;
       }

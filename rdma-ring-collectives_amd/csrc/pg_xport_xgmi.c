@@ -124,6 +124,21 @@ static void unmap(struct pg *pg, struct xg_region *g) {
  * So the replacement is allocated and exported while every old import is
  * still mapped, and the old allocation is freed only after all ranks have
  * dropped their mappings of it. */
+/* Every rank learns whether every rank's step succeeded (one TCP all-gather). */
+static int all_ranks_ok(struct pg *pg, int ok) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  char mine = (char)(ok != 0), all[16];
+  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, 1)) return 0;
+  for (int q = 0; q < pg->world_size; ++q)
+    if (!all[q]) return 0;
+  return 1;
+}
+
+struct xg_export {
+  hipIpcMemHandle_t h;
+  int32_t ok;
+};
+
 static int ensure(struct pg *pg, int reg, size_t bytes) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xg_region *g = &ctx_of(pg)->reg[reg];
@@ -132,41 +147,60 @@ static int ensure(struct pg *pg, int reg, size_t bytes) {
   while (cap < bytes) cap *= 2;
   pg_trace(pg, "xgmi ensure: region %d grows %zu -> %zu bytes per slot", reg, g->cap, cap);
   if (g->mem && barrier(pg)) return -1;      /* nobody still reads the old slots */
+  /* allocate and export; every rank learns whether every rank managed to
+   * before anything is torn down, so a failure (out of memory) is collective */
   void *fresh = NULL;
-  PG_CHECK_HIP(hipMalloc(&fresh, ipc_safe_size(cap * 2)));
-  pg_trace(pg, "xgmi ensure: allocated");
-  hipIpcMemHandle_t mine, *all = (hipIpcMemHandle_t *)malloc(sizeof(hipIpcMemHandle_t) * (size_t)pg->world_size);
-  if (!all) { hipFree(fresh); pg_set_error("xgmi: out of host memory"); return -1; }
-  hipError_t e = hipIpcGetMemHandle(&mine, fresh);
-  if (e != hipSuccess) {
-    free(all);
-    hipFree(fresh);
-    pg_set_error("xgmi: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+  struct xg_export mine, all[16];
+  memset(&mine, 0, sizeof(mine));
+  hipError_t e = hipMalloc(&fresh, ipc_safe_size(cap * 2));
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, fresh);
+  mine.ok = e == hipSuccess;
+  if (!mine.ok) {
+    (void)hipGetLastError();
+    pg_set_error("xgmi: allocating/exporting %zu bytes of slots: %s", cap * 2, hipGetErrorString(e));
+  }
+  pg_trace(pg, "xgmi ensure: allocated and exported: %d", mine.ok);
+  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) {
+    if (fresh) hipFree(fresh);
     return -1;
   }
-  pg_trace(pg, "xgmi ensure: exported");
+  int ok = 1;
+  for (int q = 0; q < pg->world_size; ++q) ok &= all[q].ok;
+  if (!ok) {
+    if (fresh) hipFree(fresh);
+    if (mine.ok) pg_set_error("xgmi: a peer could not allocate %zu bytes of exchange slots", cap * 2);
+    return -1;                                /* the old slots stay as they were, on every rank */
+  }
   if (g->mem) {
     unmap_peers(pg, g);
     pg_trace(pg, "xgmi ensure: old peer slots unmapped");
-    if (barrier(pg)) { free(all); hipFree(fresh); return -1; }   /* nobody maps my old slots */
+    if (barrier(pg)) { hipFree(fresh); return -1; }   /* nobody maps my old slots */
     hipFree(g->mem);
     pg_trace(pg, "xgmi ensure: old slots freed");
   }
   g->mem = fresh;
   g->cap = cap;
   g->peer[pg->rank] = g->mem;
-  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) { free(all); return -1; }
-  for (int q = 0; q < pg->world_size; ++q) {
+  int opened = 1;
+  for (int q = 0; q < pg->world_size && opened; ++q) {
     if (q == pg->rank) continue;
-    e = hipIpcOpenMemHandle(&g->peer[q], all[q], hipIpcMemLazyEnablePeerAccess);
+    e = hipIpcOpenMemHandle(&g->peer[q], all[q].h, hipIpcMemLazyEnablePeerAccess);
     pg_trace(pg, "xgmi ensure: opened rank %d's slots: %s", q, hipGetErrorString(e));
     if (e != hipSuccess) {
-      free(all);
+      g->peer[q] = NULL;
       pg_set_error("xgmi: hipIpcOpenMemHandle(rank %d): %s", q, hipGetErrorString(e));
-      return -1;
+      opened = 0;
     }
   }
-  free(all);
+  if (!all_ranks_ok(pg, opened)) {
+    /* undo on every rank: nobody keeps a region some peer cannot reach */
+    unmap_peers(pg, g);
+    if (barrier(pg) == 0) hipFree(g->mem);
+    g->mem = NULL;
+    g->cap = 0;
+    if (opened) pg_set_error("xgmi: a peer could not map this rank's exchange slots");
+    return -1;
+  }
   return 0;
 }
 
