@@ -4,7 +4,8 @@
 //  - one-shot tiles (as shipped) with the workgroups per CU capped by a
 //    dynamic LDS reservation (no LDS is touched; the reservation only limits
 //    how many workgroups a CU holds, i.e. the HBM requests in flight per CU);
-//  - a persistent grid whose threads load tile t + grid before storing tile t.
+//  - a persistent grid whose threads load tile t + grid before storing tile t;
+//  - LDS-DMA staging of both operands (global_load_lds_dwordx4 -> ds_read_b128).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -41,9 +42,31 @@ __global__ __launch_bounds__(B) void persist(f64x2* __restrict__ d, const f64x2*
   }
 }
 
+// LDS staging: both operands land in LDS by LDS-DMA (global_load_lds_dwordx4,
+// nt), each wave reads back its own 64 lanes' vectors (ds_read_b128), adds,
+// and stores from registers.  LDS destination is wave-uniform base + lane*16.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+template <int B, int U>
+__global__ __launch_bounds__(B) void glds(f64x2* __restrict__ d, const f64x2* __restrict__ s) {
+  __shared__ f64x2 la[B * U], lb[B * U];
+  const size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+  const int w = threadIdx.x / 64;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    __builtin_amdgcn_global_load_lds((glb_void*)(d + base + u * B), (lds_void*)(la + u * B + w * 64), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((glb_void*)(s + base + u * B), (lds_void*)(lb + u * B + w * 64), 16, 0, 2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    __builtin_nontemporal_store(la[u * B + threadIdx.x] + lb[u * B + threadIdx.x], d + base + u * B);
+}
+
 struct V {
   const char* name;
-  int kind;        // 0 oneshot, 1 persist
+  int kind;        // 0 oneshot, 1 persist, 2 LDS-DMA staged oneshot
   int block, unroll, lds_kib, per_cu;
 };
 
@@ -62,6 +85,9 @@ static const V kV[] = {
     {"oneshot 256x4 lds0", 0, 256, 4, 0, 0},
     {"oneshot 256x8 lds0", 0, 256, 8, 0, 0},
     {"oneshot 512x4 lds0", 0, 512, 4, 0, 0},
+    {"glds (LDS-DMA staged) 1024x1", 2, 1024, 1, 0, 0},
+    {"glds (LDS-DMA staged) 512x2", 2, 512, 2, 0, 0},
+    {"glds (LDS-DMA staged) 256x4", 2, 256, 4, 0, 0},
     {"persist 1024 x2/CU", 1, 1024, 1, 0, 2},
     {"persist 1024 x1/CU", 1, 1024, 1, 0, 1},
     {"persist 512 x4/CU", 1, 512, 1, 0, 4},
@@ -102,6 +128,14 @@ extern "C" int lab2_launch(int vi, double* d, const double* s, size_t n, void* s
       case 256 * 16 + 2: go1<256, 2>(v, vd, vs, nvec, st); break;
       case 256 * 16 + 4: go1<256, 4>(v, vd, vs, nvec, st); break;
       case 256 * 16 + 8: go1<256, 8>(v, vd, vs, nvec, st); break;
+      default: return -5;
+    }
+  } else if (v.kind == 2) {
+    size_t grid = nvec / (v.block * v.unroll);
+    switch (v.block) {
+      case 1024: hipLaunchKernelGGL((glds<1024, 1>), dim3((unsigned)grid), dim3(1024), 0, st, vd, vs); break;
+      case 512: hipLaunchKernelGGL((glds<512, 2>), dim3((unsigned)grid), dim3(512), 0, st, vd, vs); break;
+      case 256: hipLaunchKernelGGL((glds<256, 4>), dim3((unsigned)grid), dim3(256), 0, st, vd, vs); break;
       default: return -5;
     }
   } else {
