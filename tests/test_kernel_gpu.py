@@ -253,3 +253,29 @@ def test_fold_blocks_and_gather(gpu, lib, oracle):
     assert np.array_equal(got, want)
     bad = (ctypes.c_size_t * 1)(3)
     assert lib.pgk_gather(ds, ss, bad, 1, stream(torch)) == -1
+
+
+def test_reduce_captured_in_hip_graph(gpu, lib, oracle):
+    """include/pgk.h promises pgk_reduce allocates nothing and is safe to
+    capture: a chain of reduces captured into a hipGraph (torch.cuda.CUDAGraph
+    is hipGraph on ROCm) and replayed three times gives the oracle's result of
+    the same chain applied three times, bit for bit."""
+    torch = gpu
+    n = (1 << 20) + 5
+    for dt, op in ((1, 0), (0, 1)):
+        a, b, c = (oracle.fill(n, dt, op, 60 + k) for k in range(3))
+        A, B, C = to_dev(torch, a), to_dev(torch, b), to_dev(torch, c)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                sh = torch.cuda.current_stream().cuda_stream
+                assert lib.pgk_reduce(ptr(A), ptr(B), n, dt, op, sh) == 0      # A op= B
+                assert lib.pgk_reduce(ptr(A), ptr(C), n, dt, op, sh) == 0      # A op= C
+        want = a.copy()
+        for _ in range(3):
+            g.replay()
+            want = oracle.reduce(oracle.reduce(want, b, dt, op), c, dt, op)
+        torch.cuda.synchronize()
+        assert to_host(torch, A).tobytes() == want.tobytes(), (dt, op)
