@@ -120,13 +120,17 @@ __global__ __launch_bounds__(kScalarBlock) void k_reduce_scalar(T* __restrict__ 
 // the same order.  Sources are passed by value in the kernel arguments.
 constexpr int kMaxSrc = 16;
 constexpr int kMultiBlock = 256;
+// The vector fold streams k sources + 1 output.  Block shapes of 256, 512 and
+// 1024 threads measure within run-to-run noise of each other (5.6-6.3 TB/s of
+// 9 x 64 MiB .. 9 x 1 GiB at k = 8, profiles/r01_lab3_fold.txt); 512 is the middle.
+constexpr int kMultiVecBlock = 512;
 template <typename T>
 struct SrcList {
   const T* p[kMaxSrc];
 };
 
 template <typename T, int OP, int NS>
-__global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_vec(T* __restrict__ out, SrcList<T> src,
+__global__ __launch_bounds__(kMultiVecBlock) void k_reduce_multi_vec(T* __restrict__ out, SrcList<T> src,
                                                                   int nsrc, unsigned head, size_t nvec,
                                                                   unsigned tail) {
   using V = typename VecOf<T>::type;
@@ -138,21 +142,29 @@ __global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_vec(T* __restrict_
     for (int j = 1; j < k; ++j) acc = apply<OP>(acc, src.p[j][e]);
     out[e] = acc;
   }
-  const size_t stride = (size_t)gridDim.x * kMultiBlock;
-  for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < nvec; i += stride) {
-    if constexpr (NS > 0) {
+  const size_t stride = (size_t)gridDim.x * kMultiVecBlock;
+  size_t i = (size_t)blockIdx.x * kMultiVecBlock + threadIdx.x;
+  if constexpr (NS > 0) {
+    const V* vs[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) vs[j] = reinterpret_cast<const V*>(src.p[j] + head);
+    V* vo = reinterpret_cast<V*>(out + head);
+    // one vector per thread: the grid covers nvec except past 2^32 work-items
+    for (; i < nvec; i += stride) {
       V x[NS];
 #pragma unroll
-      for (int j = 0; j < NS; ++j) x[j] = ld<true>(reinterpret_cast<const V*>(src.p[j] + head) + i);
+      for (int j = 0; j < NS; ++j) x[j] = ld<true>(vs[j] + i);
       V acc = x[0];
 #pragma unroll
       for (int j = 1; j < NS; ++j) acc = apply<OP>(acc, x[j]);
-      st<true>(reinterpret_cast<V*>(out + head) + i, acc);
-    } else {
-      V acc = ld<true>(reinterpret_cast<const V*>(src.p[0] + head) + i);
-      for (int j = 1; j < k; ++j) acc = apply<OP>(acc, ld<true>(reinterpret_cast<const V*>(src.p[j] + head) + i));
-      st<true>(reinterpret_cast<V*>(out + head) + i, acc);
+      st<true>(vo + i, acc);
     }
+    return;
+  }
+  for (; i < nvec; i += stride) {          // nsrc > 8: sources in a runtime loop
+    V acc = ld<true>(reinterpret_cast<const V*>(src.p[0] + head) + i);
+    for (int j = 1; j < k; ++j) acc = apply<OP>(acc, ld<true>(reinterpret_cast<const V*>(src.p[j] + head) + i));
+    st<true>(reinterpret_cast<V*>(out + head) + i, acc);
   }
 }
 
@@ -385,10 +397,10 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
     size_t head = m ? (16 - m) / sizeof(T) : 0;
     if (head > n) head = n;
     size_t nvec = (n - head) / W, tail = (n - head) % W;
-    size_t g = (nvec + kMultiBlock - 1) / kMultiBlock;
+    size_t g = (nvec + kMultiVecBlock - 1) / kMultiVecBlock;
     if (g == 0) g = 1;
-    if (g > grid_cap(kMultiBlock)) g = grid_cap(kMultiBlock);
-    dim3 grid((unsigned)g), block(kMultiBlock);
+    if (g > grid_cap(kMultiVecBlock)) g = grid_cap(kMultiVecBlock);
+    dim3 grid((unsigned)g), block(kMultiVecBlock);
     switch (nsrc) {
 #define PGK_MULTI_CASE(K) \
       case K: hipLaunchKernelGGL((k_reduce_multi_vec<T, OP, K>), grid, block, 0, s, out, sl, nsrc, \
