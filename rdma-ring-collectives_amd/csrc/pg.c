@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "pg_impl.h"
 
@@ -37,24 +38,37 @@ void pg_set_error(const char *fmt, ...) {
 
 const char *pg_last_error(void) { return g_pg_err; }
 
-/* PG_TRACE=1: one stderr line per transport phase (rank, monotonic ms), to
- * name the phase a stalled multi-process call is in. */
+/* PG_TRACE=1: one stderr line per transport phase (rank, monotonic time), to
+ * name the phase a stalled multi-process call is in.  PG_TRACE_FILE=prefix
+ * instead writes them, fully buffered, to prefix.<pid> (flushed at exit): far
+ * less perturbation when chasing a timing-dependent fault. */
+static FILE *g_trace = NULL;
+static int g_trace_on = -1;
+
 void pg_trace(const struct pg *pg, const char *fmt, ...) {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("PG_TRACE");
-    on = e && *e == '1';
+  if (g_trace_on < 0) {
+    const char *f = getenv("PG_TRACE_FILE"), *e = getenv("PG_TRACE");
+    g_trace_on = 0;
+    if (f && *f) {
+      char path[512];
+      snprintf(path, sizeof(path), "%s.%d", f, (int)getpid());
+      g_trace = fopen(path, "w");
+      if (g_trace) { setvbuf(g_trace, NULL, _IOFBF, 1 << 20); g_trace_on = 1; }
+    } else if (e && *e == '1') {
+      g_trace = stderr;
+      g_trace_on = 1;
+    }
   }
-  if (!on) return;
-  char msg[256];
+  if (!g_trace_on) return;
+  char msg[320];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(msg, sizeof(msg), fmt, ap);
   va_end(ap);
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
-  fprintf(stderr, "[pg r%d %ld.%03ld] %s\n", pg ? pg->rank : -1, (long)ts.tv_sec, ts.tv_nsec / 1000000L, msg);
-  fflush(stderr);
+  fprintf(g_trace, "[pg r%d %ld.%06ld] %s\n", pg ? pg->rank : -1, (long)ts.tv_sec, ts.tv_nsec / 1000L, msg);
+  if (g_trace == stderr) fflush(stderr);
 }
 
 /* ---- small helpers ---------------------------------------------------------- */

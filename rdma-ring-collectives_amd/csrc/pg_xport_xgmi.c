@@ -37,10 +37,17 @@
 
 struct xg_import {
   unsigned long long bid;
-  void *base;
+  uint64_t peer_base;           /* the allocation's address range in the      */
+  uint64_t peer_size;           /* exporter                                   */
+  void *base;                   /* its mapping here                           */
   unsigned long stamp;
 };
 #define XG_GRANULE (64ull << 20)
+
+struct xg_hist {
+  uint64_t base, size;
+  unsigned long long bid;
+};
 
 struct xg_region {
   void *mem;                    /* my allocation: 2 slots of cap bytes      */
@@ -58,6 +65,8 @@ struct xgmi_ctx {
   unsigned long long exp_bid;
   void *exp_base;
   int exp_valid;
+  struct xg_hist *hist;         /* every allocation ever exported (see export_input) */
+  size_t nhist, hist_cap;
   struct xg_import *imp;        /* world * XG_IMPORTS mapped peer inputs     */
   unsigned long clock;
   unsigned long gen;            /* collective calls so far (slot parity)    */
@@ -242,6 +251,7 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   if ((x->reg[XG_REG_X].mem || x->reg[XG_REG_R].mem) && im->boot_fds) barrier(pg);
   drop_imports(pg, x);
   free(x->imp);
+  free(x->hist);
   for (int g = 0; g < 2; ++g) {
     unmap(pg, &x->reg[g]);
     free(x->reg[g].peer);
@@ -274,13 +284,56 @@ static int is_dev(const void *p) {
 struct xg_desc {
   hipIpcMemHandle_t h;
   uint64_t bid;                  /* HIP buffer id of the exported allocation */
+  uint64_t base;                 /* its base address in the exporter          */
+  uint64_t size;                 /* and its size                              */
   uint64_t off;                  /* input offset inside it                    */
+  uint64_t nbytes;               /* the call's input bytes (must agree)       */
   int32_t ok;
   int32_t pad;
 };
 
+/* call-result flags, double-buffered by call parity, after the descriptors */
+#define XG_FLAG_OFF (XG_DESC_OFF + 16 * (int)sizeof(struct xg_desc))
+_Static_assert(XG_FLAG_OFF + 2 * 16 * 4 <= 4096, "shm page layout");
+
 static struct xg_desc *descs(struct xgmi_ctx *x) {
   return (struct xg_desc *)((char *)x->bar + XG_DESC_OFF);
+}
+
+/* An IPC handle names (exporter pid, address, size), not the allocation
+ * (tools/ipc_probe4.py: a new allocation at a freed one's address exports
+ * byte-identical handle bytes), and what hipIpcOpenMemHandle does in an
+ * importer that opened that range before is not something this transport can
+ * control: it may hand back a mapping of the freed allocation (stale data,
+ * tools/xgmi_cfg5_probe.py and tests/test_xgmi_gpu.py::
+ * test_xgmi_input_reallocated_at_same_address reproduced it), and it failed
+ * once in 226 calls of the cfg5 probe.  So an allocation whose address range
+ * overlaps one this rank exported earlier under another buffer id is never
+ * exported: the call takes the slot copy instead.  Buffer ids are never
+ * reused, so the history check is exact. */
+static int range_was_exported(struct xgmi_ctx *x, uint64_t base, uint64_t size, unsigned long long bid, int *seen) {
+  *seen = 0;
+  for (size_t i = 0; i < x->nhist; ++i) {
+    const struct xg_hist *h = &x->hist[i];
+    if (h->bid == bid) { *seen = 1; continue; }
+    if (h->base < base + size && base < h->base + h->size) return 1;
+  }
+  return 0;
+}
+
+static int remember_export(struct xgmi_ctx *x, uint64_t base, uint64_t size, unsigned long long bid) {
+  if (x->nhist == x->hist_cap) {
+    size_t cap = x->hist_cap ? 2 * x->hist_cap : 64;
+    struct xg_hist *n = (struct xg_hist *)realloc(x->hist, cap * sizeof(*n));
+    if (!n) return -1;
+    x->hist = n;
+    x->hist_cap = cap;
+  }
+  x->hist[x->nhist].base = base;
+  x->hist[x->nhist].size = size;
+  x->hist[x->nhist].bid = bid;
+  ++x->nhist;
+  return 0;
 }
 
 static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
@@ -295,36 +348,55 @@ static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
   }
   if (!ipc_size_ok(size)) return 0;           /* peers could not open it: slot copy */
   if (!x->exp_valid || x->exp_bid != bid || x->exp_base != base) {
+    int seen;
+    if (range_was_exported(x, (uint64_t)(uintptr_t)base, (uint64_t)size, bid, &seen)) return 0;
     x->exp_valid = 0;
     if (hipIpcGetMemHandle(&x->exp_h, base) != hipSuccess) { (void)hipGetLastError(); return 0; }
+    if (!seen && remember_export(x, (uint64_t)(uintptr_t)base, (uint64_t)size, bid)) return 0;
     x->exp_bid = bid;
     x->exp_base = base;
     x->exp_valid = 1;
   }
   d->h = x->exp_h;
   d->bid = bid;
+  d->base = (uint64_t)(uintptr_t)base;
+  d->size = (uint64_t)size;
   d->off = (uint64_t)((const char *)in - (const char *)base);
   d->ok = 1;
   return 1;
 }
 
-/* Peer q's input, mapped (LRU cache of XG_IMPORTS allocations per peer). */
+/* Peer q's input, mapped (LRU cache of XG_IMPORTS allocations per peer).  On
+ * a miss, any cached mapping of this peer whose exporter range overlaps the
+ * new one is closed first (its allocation has been freed: live allocations do
+ * not overlap); with export_input's rule this should never find one. */
 static const char *import_input(struct xgmi_ctx *x, int q, const struct xg_desc *d) {
   struct xg_import *e = &x->imp[q * XG_IMPORTS];
-  int lru = 0;
   ++x->clock;
-  for (int i = 0; i < XG_IMPORTS; ++i) {
+  for (int i = 0; i < XG_IMPORTS; ++i)
     if (e[i].base && e[i].bid == d->bid) { e[i].stamp = x->clock; return (const char *)e[i].base + d->off; }
+  for (int i = 0; i < XG_IMPORTS; ++i)
+    if (e[i].base && e[i].peer_base < d->base + d->size && d->base < e[i].peer_base + e[i].peer_size) {
+      hipIpcCloseMemHandle(e[i].base);
+      e[i].base = NULL;
+      e[i].stamp = 0;
+    }
+  int lru = 0;
+  for (int i = 1; i < XG_IMPORTS; ++i)
     if (e[i].stamp < e[lru].stamp) lru = i;
-  }
   if (e[lru].base) { hipIpcCloseMemHandle(e[lru].base); e[lru].base = NULL; }
   void *p = NULL;
-  if (hipIpcOpenMemHandle(&p, d->h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+  hipError_t err = hipIpcOpenMemHandle(&p, d->h, hipIpcMemLazyEnablePeerAccess);
+  if (err != hipSuccess) {
     (void)hipGetLastError();
+    pg_set_error("xgmi: hipIpcOpenMemHandle(rank %d's input, bid %llu): %s", q, (unsigned long long)d->bid,
+                 hipGetErrorString(err));
     return NULL;
   }
   e[lru].base = p;
   e[lru].bid = d->bid;
+  e[lru].peer_base = d->base;
+  e[lru].peer_size = d->size;
   e[lru].stamp = x->clock;
   return (const char *)p + d->off;
 }
@@ -352,22 +424,41 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   if (x->zc && x->bar && bytes) {
     struct xg_desc mine;
     if (!in_dev || may_alias_out || !export_input(x, in, &mine)) memset(&mine, 0, sizeof(mine));
-    pg_trace(pg, "xgmi share: input %p exported=%d", in, mine.ok);
+    mine.nbytes = bytes;
+    pg_trace(pg, "xgmi share: input %p exported=%d (bid %llu base %#llx size %llu)", in, mine.ok,
+             (unsigned long long)mine.bid, (unsigned long long)mine.base, (unsigned long long)mine.size);
     descs(x)[r] = mine;
     if (barrier(pg)) return -1;
     struct xg_desc all[16];
     memcpy(all, descs(x), sizeof(struct xg_desc) * (size_t)W);
-    int all_ok = 1;
-    for (int q = 0; q < W; ++q) all_ok &= all[q].ok;
+    int all_ok = 1, agree = 1;
+    for (int q = 0; q < W; ++q) {
+      agree &= all[q].nbytes == bytes;
+      all_ok &= all[q].ok && all[q].off <= all[q].size && bytes <= all[q].size - all[q].off;
+    }
+    pg_trace(pg, "xgmi share: call %lu, %zu bytes, zero-copy %d", x->gen, bytes, all_ok);
+    if (!agree) {
+      /* ranks called with different counts (or types): every rank sees the same
+       * table, so every rank fails this call here -- before any peer memory is
+       * read with the wrong extent.  Meet once more so that nobody rewrites the
+       * table before all have read it. */
+      for (int q = 0; q < W; ++q)
+        if (all[q].nbytes != bytes) {
+          pg_set_error("xgmi: rank %d called with %llu bytes, this rank with %zu (counts must agree)", q,
+                       (unsigned long long)all[q].nbytes, bytes);
+          break;
+        }
+      barrier(pg);
+      return -1;
+    }
     im->stats.barrier_us += us_now() - t1;
     if (all_ok) {
       for (int q = 0; q < W; ++q) {
         by_rank[q] = q == r ? (const char *)in : import_input(x, q, &all[q]);
-        pg_trace(pg, "xgmi share: rank %d's input at %p", q, (const void *)by_rank[q]);
-        if (!by_rank[q]) {
-          pg_set_error("xgmi: could not map rank %d's input", q);
-          *fail = 1;
-        }
+        pg_trace(pg, "xgmi share: rank %d's input at %p (bid %llu base %#llx size %llu off %llu)", q,
+                 (const void *)by_rank[q], (unsigned long long)all[q].bid, (unsigned long long)all[q].base,
+                 (unsigned long long)all[q].size, (unsigned long long)all[q].off);
+        if (!by_rank[q]) *fail = 1;           /* error set by import_input */
       }
       *zero_copy = 1;
       return 0;
@@ -377,6 +468,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   /* every rank reaches this point in this call (the choice above is collective) */
   if (bytes && ensure(pg, XG_REG_X, bytes)) return -1;
   char *xs = slot(x, XG_REG_X, r, which);
+  pg_trace(pg, "xgmi share: call %lu slot copy of %zu bytes into X%d at %p", x->gen, bytes, which, (void *)xs);
   double t2 = us_now();
   if (bytes) {
     if (in_dev && ((uintptr_t)in & 3) == 0 && (bytes & 3) == 0) {
@@ -401,18 +493,25 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   return rc;
 }
 
-/* End of a call: zero-copy inputs stay untouched until every peer is done. */
+/* End of a call: zero-copy inputs stay untouched until every peer is done.
+ * That closing barrier also carries each rank's result, so a rank that could
+ * not map a peer or launch its fold fails the call on every rank: callers see
+ * the same return code everywhere and stay in step. */
 static int finish(struct pg *pg, int zero_copy, int fail) {
   struct xgmi_ctx *x = ctx_of(pg);
-  int rc = 0;
+  int rc = 0, any = fail;
   if (zero_copy) {
     struct pg_impl *im = (struct pg_impl *)pg->impl;
+    volatile int32_t *flags = (volatile int32_t *)((char *)x->bar + XG_FLAG_OFF) + (x->gen & 1) * 16;
+    flags[pg->rank] = fail;
     double t = us_now();
     rc = barrier(pg);
     im->stats.barrier_us += us_now() - t;
+    for (int q = 0; q < pg->world_size && !rc; ++q) any |= flags[q];
+    if (any && !fail && !rc) pg_set_error("xgmi: a peer failed this call");
   }
   x->gen++;
-  return (rc || fail) ? -1 : 0;
+  return (rc || any) ? -1 : 0;
 }
 
 /* out = fold over ranks of this rank's block (at off_elems, len elements),
@@ -434,6 +533,7 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
     for (int j = 0; j < W; ++j) {
       int q = g == 0 ? (r + 1 + j) % W : ((r - 1 - j) % W + W) % W;
       srcs[j] = by_rank[q] + (off_elems + po) * es;
+      pg_trace(pg, "xgmi fold: part %d source %d = rank %d at %p", g, j, q, srcs[j]);
     }
     if (pgk_reduce_multi((char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red)) {
       pg_set_error("xgmi: %s", pgk_last_error());
@@ -484,11 +584,20 @@ static int push_inputs(struct pg *pg, const char *in, int count, int dt, int can
   struct xg_desc mine;
   memset(&mine, 0, sizeof(mine));
   mine.ok = can && ((uintptr_t)in & 3) == 0;
+  mine.nbytes = (size_t)count * es;
   descs(x)[r] = mine;
   if (barrier(pg)) return -1;
-  int all_ok = 1;
-  for (int q = 0; q < W; ++q) all_ok &= descs(x)[q].ok;
+  int all_ok = 1, agree = 1;
+  for (int q = 0; q < W; ++q) {
+    all_ok &= descs(x)[q].ok;
+    agree &= descs(x)[q].nbytes == mine.nbytes;
+  }
   im->stats.barrier_us += us_now() - t1;
+  if (!agree) {                                  /* as in share_inputs: everybody fails here */
+    pg_set_error("xgmi: ranks called with different counts (counts must agree)");
+    barrier(pg);
+    return -1;
+  }
   if (!all_ok) {
     /* everybody takes the read path, whose first step rewrites the descriptor
      * page: meet once more so that no rank does so before all have read it */

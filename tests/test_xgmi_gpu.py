@@ -313,3 +313,133 @@ def test_xgmi_link_probe(gpu, world):
         assert "exception" not in out, out
         assert out["rc"] == 0 and all(v > 0 for v in out["gbs"]), (rank, out)
         assert out["bad_rc"] == -1
+
+
+def _realloc_worker(rank, world, port, q):
+    """A rank frees its input allocation and makes a new one, which lands at the
+    same address (hipMalloc reuses it for equal sizes); the IPC handle of the
+    new allocation is byte-identical to the old one's (tools/ipc_probe4.py), so
+    a peer that kept its mapping of the old allocation would be handed that
+    stale mapping back by hipIpcOpenMemHandle and fold freed data."""
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="60000")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    out = {"fails": [], "same_va": None}
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        hip.hipFree.argtypes = [ctypes.c_void_p]
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        count = 8 << 20                                            # 64 MiB of doubles
+        off, ln = pgamd.block_range(count, world, rank)
+        vas = []
+        for trial in range(3):
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), count * 8) == 0
+            vas.append(p.value)
+            x = (np.arange(count, dtype=np.float64) % 97) + 1000 * trial + rank
+            assert hip.hipMemcpy(p, x.ctypes.data, count * 8, 1) == 0      # hipMemcpyHostToDevice
+            y = torch.empty(ln, dtype=torch.float64, device="cuda")
+            if lib.pg_reduce_scatter(p.value, y.data_ptr(), count, 1, 0, h) != 0:
+                out["fails"].append((trial, pgamd.last_error()))
+            i = np.arange(off, off + ln)
+            want = world * (i % 97) + world * 1000 * trial + world * (world - 1) // 2
+            if not np.array_equal(y.cpu().numpy(), want.astype(np.float64)):
+                out["fails"].append((trial, "stale or wrong data"))
+            hip.hipFree(p)
+        out["same_va"] = len(set(vas)) < len(vas)
+        lib.pg_close(h)
+    except Exception as e:
+        out["fails"].append(("exception", repr(e)))
+    q.put((rank, out))
+
+
+def test_xgmi_input_reallocated_at_same_address(gpu):
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_realloc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=150))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, out in results:
+        assert not out["fails"], (rank, out)
+    assert any(out["same_va"] for _, out in results), "no address was reused: the test did not set up the hazard"
+
+
+def _mismatch_worker(rank, world, port, q, mode):
+    """Rank 1 passes a different count than the others.  Every rank must fail
+    that call (the descriptors carry each rank's byte count) before any peer
+    memory is read with the wrong extent, and the ranks must stay in step: the
+    next, well-formed call succeeds everywhere with the right answer."""
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE=mode)
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    out = {"rcs": [], "fails": []}
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        x = torch.full((4096,), rank + 1, dtype=torch.int32, device="cuda")
+        y = torch.zeros(4096, dtype=torch.int32, device="cuda")
+        bad = 512 if rank == 1 else 256
+        out["rcs"].append(lib.pg_reduce_scatter(x.data_ptr(), y.data_ptr(), bad, 0, 0, h))
+        out["err"] = pgamd.last_error()
+        out["rcs"].append(lib.pg_all_reduce(x.data_ptr(), y.data_ptr(), bad, 0, 0, h))
+        out["rcs"].append(lib.pg_reduce_scatter(x.data_ptr(), y.data_ptr(), 3000, 0, 0, h))
+        off, ln = pgamd.block_range(3000, world, rank)
+        if not torch.equal(y[:ln].cpu(), torch.full((ln,), world * (world + 1) // 2, dtype=torch.int32)):
+            out["fails"].append("wrong result after the failed calls")
+        lib.pg_close(h)
+    except Exception as e:
+        out["fails"].append(repr(e))
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("mode", ["read", "push"])
+def test_xgmi_count_mismatch_fails_on_every_rank(gpu, mode):
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=150))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, out in results:
+        assert not out["fails"] and out["rcs"] == [-1, -1, 0], (rank, out)
+        assert "counts must agree" in out["err"], (rank, out)
