@@ -138,9 +138,15 @@ def kernel_leg(lib, args, rank, world):
     launch duration over them (HIP events bracketing the timed region on the
     launch stream, / K), and kernel-stamped per-launch durations from an
     untimed cross-check pass."""
+    # one allocation carved into N_PAIRS adjacent (dst, src) pairs, as the size
+    # table does: operand placement moves this kernel by 1-5 % (DESIGN.md §4,
+    # "placement"), and separate torch allocations land wherever the caching
+    # allocator puts them, so the primary figure would depend on what ran before
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
-    dst = [torch.rand(N_ELEMS, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(N_PAIRS)]
-    src = [torch.rand(N_ELEMS, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(N_PAIRS)]
+    pool = torch.empty(2 * N_PAIRS * N_ELEMS, dtype=torch.float64, device="cuda")
+    pool.uniform_(-1.0, 1.0, generator=g)
+    dst = [pool[(2 * i) * N_ELEMS:(2 * i + 1) * N_ELEMS] for i in range(N_PAIRS)]
+    src = [pool[(2 * i + 1) * N_ELEMS:(2 * i + 2) * N_ELEMS] for i in range(N_PAIRS)]
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
@@ -181,7 +187,7 @@ def kernel_leg(lib, args, rank, world):
         stamped.append(ms.value)
         lib.pgk_event_destroy(a)
         lib.pgk_event_destroy(b)
-    del dst, src
+    del dst, src, pool
     torch.cuda.empty_cache()
     return t1 - t0, region_mean_ms, stamped
 
@@ -734,7 +740,7 @@ def main():
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (uniform [-1,1) doubles, HBM-resident, 4 rotating 256 MiB dst/src pairs)",
+            "data": "synthetic (uniform [-1,1) doubles, HBM-resident, 4 rotating 256 MiB dst/src pairs carved from one 2 GiB allocation)",
             "config": {"workload": "BASELINE config 2: pgk_reduce DT_DOUBLE OP_SUM, 256 MiB chunk per GPU "
                                    "(dst op= src), one reduce per step per GPU",
                        "chunk_bytes": N_ELEMS * 8, "bytes_per_step_per_gpu": bytes_per_step,
