@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include <time.h>
 
 #include "pg_impl.h"
@@ -65,8 +66,6 @@ struct xgmi_ctx {
   unsigned long long exp_bid;
   void *exp_base;
   int exp_valid;
-  struct xg_hist *hist;         /* every allocation ever exported (see export_input) */
-  size_t nhist, hist_cap;
   struct xg_import *imp;        /* world * XG_IMPORTS mapped peer inputs     */
   unsigned long clock;
   unsigned long gen;            /* collective calls so far (slot parity)    */
@@ -251,7 +250,6 @@ void pg_xport_xgmi_destroy(struct pg *pg) {
   if ((x->reg[XG_REG_X].mem || x->reg[XG_REG_R].mem) && im->boot_fds) barrier(pg);
   drop_imports(pg, x);
   free(x->imp);
-  free(x->hist);
   for (int g = 0; g < 2; ++g) {
     unmap(pg, &x->reg[g]);
     free(x->reg[g].peer);
@@ -308,32 +306,44 @@ static struct xg_desc *descs(struct xgmi_ctx *x) {
  * tools/xgmi_cfg5_probe.py and tests/test_xgmi_gpu.py::
  * test_xgmi_input_reallocated_at_same_address reproduced it), and it failed
  * once in 226 calls of the cfg5 probe.  So an allocation whose address range
- * overlaps one this rank exported earlier under another buffer id is never
+ * overlaps one this process exported earlier under another buffer id is never
  * exported: the call takes the slot copy instead.  Buffer ids are never
  * reused, so the history check is exact. */
-static int range_was_exported(struct xgmi_ctx *x, uint64_t base, uint64_t size, unsigned long long bid, int *seen) {
-  *seen = 0;
-  for (size_t i = 0; i < x->nhist; ++i) {
-    const struct xg_hist *h = &x->hist[i];
-    if (h->bid == bid) { *seen = 1; continue; }
-    if (h->base < base + size && base < h->base + h->size) return 1;
-  }
-  return 0;
-}
+/* The history is per process, not per handle: the importer-side state it
+ * guards lives in each peer's HIP runtime and outlives a pg handle. */
+static struct {
+  pthread_mutex_t mu;
+  struct xg_hist *v;
+  size_t n, cap;
+} g_exported = {PTHREAD_MUTEX_INITIALIZER, NULL, 0, 0};
 
-static int remember_export(struct xgmi_ctx *x, uint64_t base, uint64_t size, unsigned long long bid) {
-  if (x->nhist == x->hist_cap) {
-    size_t cap = x->hist_cap ? 2 * x->hist_cap : 64;
-    struct xg_hist *n = (struct xg_hist *)realloc(x->hist, cap * sizeof(*n));
-    if (!n) return -1;
-    x->hist = n;
-    x->hist_cap = cap;
+/* 1: [base, base+size) may be exported under `bid` (recorded if new); 0: it
+ * overlaps an allocation exported before under another id, or out of memory. */
+static int may_export(uint64_t base, uint64_t size, unsigned long long bid) {
+  int ok = 1, seen = 0;
+  pthread_mutex_lock(&g_exported.mu);
+  for (size_t i = 0; i < g_exported.n && ok; ++i) {
+    const struct xg_hist *h = &g_exported.v[i];
+    if (h->bid == bid) seen = 1;
+    else if (h->base < base + size && base < h->base + h->size) ok = 0;
   }
-  x->hist[x->nhist].base = base;
-  x->hist[x->nhist].size = size;
-  x->hist[x->nhist].bid = bid;
-  ++x->nhist;
-  return 0;
+  if (ok && !seen) {
+    if (g_exported.n == g_exported.cap) {
+      size_t cap = g_exported.cap ? 2 * g_exported.cap : 64;
+      struct xg_hist *v = (struct xg_hist *)realloc(g_exported.v, cap * sizeof(*v));
+      if (v) { g_exported.v = v; g_exported.cap = cap; }
+    }
+    if (g_exported.n < g_exported.cap) {
+      g_exported.v[g_exported.n].base = base;
+      g_exported.v[g_exported.n].size = size;
+      g_exported.v[g_exported.n].bid = bid;
+      ++g_exported.n;
+    } else {
+      ok = 0;
+    }
+  }
+  pthread_mutex_unlock(&g_exported.mu);
+  return ok;
 }
 
 static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
@@ -348,11 +358,9 @@ static int export_input(struct xgmi_ctx *x, const void *in, struct xg_desc *d) {
   }
   if (!ipc_size_ok(size)) return 0;           /* peers could not open it: slot copy */
   if (!x->exp_valid || x->exp_bid != bid || x->exp_base != base) {
-    int seen;
-    if (range_was_exported(x, (uint64_t)(uintptr_t)base, (uint64_t)size, bid, &seen)) return 0;
+    if (!may_export((uint64_t)(uintptr_t)base, (uint64_t)size, bid)) return 0;
     x->exp_valid = 0;
     if (hipIpcGetMemHandle(&x->exp_h, base) != hipSuccess) { (void)hipGetLastError(); return 0; }
-    if (!seen && remember_export(x, (uint64_t)(uintptr_t)base, (uint64_t)size, bid)) return 0;
     x->exp_bid = bid;
     x->exp_base = base;
     x->exp_valid = 1;
