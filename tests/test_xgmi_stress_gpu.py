@@ -1,0 +1,145 @@
+"""PG_TRANSPORT=xgmi under a long random sequence of collectives in one process
+lifetime per rank: reduce-scatter / all-gather / all-reduce, int32 / double,
+sum / prod, sizes from 0 to 8 MiB, device / host / mixed buffers, in place,
+inputs that stay allocated across calls, fresh ones, and fresh allocations
+after torch.cuda.empty_cache() (which land at recycled addresses: the reuse
+hazard of DESIGN.md §5a).  Every rank draws the same sequence from one seed
+and checks every call bit for bit against the oracle's ring simulator.
+
+This is the shape of the config-5 sequence (tools/xgmi_cfg5_probe.py) that
+exposed the stale-mapping and desynchronisation bugs, widened to every call
+form and buffer kind."""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+COUNTS = (0, 1, 5, 64, 1000, 4099, 65539, 300001, (1 << 20) + 7)
+CALLS = 120
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _sequence(seed, world):
+    rng = np.random.default_rng(seed)
+    seq = []
+    for i in range(CALLS):
+        coll = ("rs", "ag", "ar")[rng.integers(3)]
+        dt, op = int(rng.integers(2)), int(rng.integers(2))
+        count = int(COUNTS[rng.integers(len(COUNTS))])
+        mem = ("dev", "dev", "dev", "host", "mixed")[rng.integers(5)]
+        in_place = coll != "rs" and rng.random() < 0.2
+        keep = rng.random() < 0.4            # reuse the previous call's input allocation if it fits
+        flush = rng.random() < 0.15          # torch.cuda.empty_cache() before this call
+        seq.append((i, coll, dt, op, count, mem, in_place, keep, flush))
+    return seq
+
+
+def _worker(rank, world, port, q, mode, seed):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE=mode)
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) != 0:
+            q.put((rank, ["connect: " + pgamd.last_error()]))
+            return
+        NP = {0: np.int32, 1: np.float64}
+        TD = {0: torch.int32, 1: torch.float64}
+        pool = None                                  # a kept device input allocation
+        for i, coll, dt, op, count, mem, in_place, keep, flush in _sequence(seed, world):
+            if flush:
+                pool = None
+                torch.cuda.empty_cache()
+            on_dev = mem == "dev" or (mem == "mixed" and rank % 2 == 0)
+            xs = [orc.fill(count, dt, op, 9000 + 31 * i + r) for r in range(world)]
+            if coll == "rs":
+                want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+                recv = np.zeros(max(want.size, 1), NP[dt])
+            elif coll == "ag":
+                want = orc.ring_all_gather(xs, dt)[rank]
+                recv = np.zeros(max(count * world, 1), NP[dt])
+                if in_place:
+                    recv[rank * count:(rank + 1) * count] = xs[rank]
+            else:
+                want = orc.ring_all_reduce(xs, dt, op)[rank]
+                recv = xs[rank].copy() if in_place else np.zeros(max(count, 1), NP[dt])
+                if recv.size == 0:
+                    recv = np.zeros(1, NP[dt])
+            send = xs[rank] if count else np.zeros(1, NP[dt])
+            if on_dev:
+                nbytes = send.nbytes
+                if keep and pool is not None and pool.numel() * pool.element_size() >= nbytes + 4096:
+                    # the same allocation as an earlier call, at an offset
+                    S = pool.view(torch.uint8)[4096:4096 + nbytes].view(TD[dt])
+                    S.copy_(torch.from_numpy(send))
+                else:
+                    pool = torch.empty((nbytes + 4096) // 4 + 1, dtype=torch.int32, device="cuda")
+                    S = pool.view(torch.uint8)[4096:4096 + nbytes].view(TD[dt])
+                    S.copy_(torch.from_numpy(send))
+                R = torch.from_numpy(recv.copy()).cuda()
+                torch.cuda.synchronize()
+                sp, rp = S.data_ptr(), R.data_ptr()
+            else:
+                S, R = send.copy(), recv.copy()
+                sp, rp = S.ctypes.data, R.ctypes.data
+            if coll == "rs":
+                rc = lib.pg_reduce_scatter(sp, rp, count, dt, op, h)
+            elif coll == "ag":
+                rc = lib.pg_all_gather(None if in_place else sp, rp, count, dt, h)
+            else:
+                rc = lib.pg_all_reduce(rp if in_place else sp, rp, count, dt, op, h)
+            if rc != 0:
+                fails.append((i, coll, count, mem, "rc", pgamd.last_error()))
+                break
+            got = R.cpu().numpy() if on_dev else R
+            if got[:want.size].tobytes() != want.tobytes():
+                fails.append((i, coll, dt, op, count, mem, in_place, keep, flush))
+        lib.pg_close(h)
+    except Exception as e:  # report, never hang the parent
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+@pytest.mark.parametrize("world,mode,seed", [(4, "read", 1), (3, "push", 2), (8, "read", 3), (5, "read", 4)])
+def test_xgmi_random_sequence(gpu, world, mode, seed):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, seed)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=420))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
