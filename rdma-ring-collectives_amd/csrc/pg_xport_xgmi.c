@@ -503,12 +503,15 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
 
 /* End of a call: zero-copy inputs stay untouched until every peer is done.
  * That closing barrier also carries each rank's result, so a rank that could
- * not map a peer or launch its fold fails the call on every rank: callers see
- * the same return code everywhere and stay in step. */
+ * not map a peer, allocate, or launch its fold fails the call on every rank:
+ * callers see the same return code everywhere and stay in step.  Slot-copy
+ * calls meet here too (one more node-local barrier, ~1 us) for the same
+ * guarantee; only the TCP-barrier fallback (PG_NO_SHM_BARRIER=1, never
+ * zero-copy) leaves a local failure local. */
 static int finish(struct pg *pg, int zero_copy, int fail) {
   struct xgmi_ctx *x = ctx_of(pg);
   int rc = 0, any = fail;
-  if (zero_copy) {
+  if (x->bar) {
     struct pg_impl *im = (struct pg_impl *)pg->impl;
     volatile int32_t *flags = (volatile int32_t *)((char *)x->bar + XG_FLAG_OFF) + (x->gen & 1) * 16;
     flags[pg->rank] = fail;
@@ -517,6 +520,8 @@ static int finish(struct pg *pg, int zero_copy, int fail) {
     im->stats.barrier_us += us_now() - t;
     for (int q = 0; q < pg->world_size && !rc; ++q) any |= flags[q];
     if (any && !fail && !rc) pg_set_error("xgmi: a peer failed this call");
+  } else if (zero_copy) {
+    rc = barrier(pg);
   }
   x->gen++;
   return (rc || any) ? -1 : 0;
@@ -657,7 +662,7 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
     return -1;
   void *out = recvbuf;
   if (!rd) {
-    if (pg_ensure(&im->dout, &im->dout_cap, len * es)) return -1;
+    if (pg_ensure(&im->dout, &im->dout_cap, len * es)) fail = 1;   /* reported by finish() on every rank */
     out = im->dout;
   }
   if (!fail && fold_block(pg, out, by_rank, fold_off, len, dt, op)) fail = 1;
@@ -704,7 +709,7 @@ int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
-    if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
+    if (pg_ensure(&im->dout, &im->dout_cap, total)) fail = 1;
     full = (char *)im->dout;
   }
   if (!fail && gather(pg, full, by_rank, count, 1, dt)) fail = 1;
@@ -732,7 +737,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
-    if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
+    if (pg_ensure(&im->dout, &im->dout_cap, bytes)) fail = 1;
     full = (char *)im->dout;
   }
   if (bytes <= x->oneshot_max) {
