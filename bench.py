@@ -521,21 +521,29 @@ def native_crosscheck(lib, h, rank, world, x_full, dt_full):
     return res
 
 
-def _one_ring(lib, rank, world, x, out, count, dt):
-    """The same timed reduce-scatter over one clockwise ring (PG_RINGS=1, a
-    second handle and RCCL communicator), to show what the counter-rotating
-    second ring buys on this node."""
+def _ring_variant(lib, rank, world, x, out, count, dt, rings, port_off):
+    """The same timed reduce-scatter with PG_RINGS=`rings` (a second handle and
+    RCCL communicator): rings = 1 shows what the counter-rotating second ring
+    buys on this node, rings = 4 what two more rings of step +3 / -3 (over
+    other xGMI links) add.  Results are checked against the default handle's."""
     saved = {k: os.environ.get(k) for k in ("PG_RINGS", "PG_PORT")}
-    os.environ["PG_RINGS"] = "1"
-    os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + 6)    # MASTER_PORT + 23: no other leg uses it
+    os.environ["PG_RINGS"] = str(rings)
+    os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + port_off)   # no other leg uses it
     h1 = ctypes.c_void_p()
     try:
         if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h1)) != 0:
             return {"error": "connect_process_group: " + pgamd.last_error()}
+        ref = out.clone()
         wall = _timed_rs(lib, h1, x, out, count, dt, pgamd.OP_SUM, 3, world)
+        same = bool(torch.equal(out, ref)) if dt == pgamd.DT_INT32 else None
         payload = count * pgamd.ELEM_SIZE[dt]
-        return {"ms_per_reduce_scatter": round(wall * 1e3, 3), "algbw_gibs": round(payload / wall / GIB, 2),
-                "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2)}
+        res = {"rings": rings, "steps": [pgamd.ring_offset(world, rings, g) for g in range(rings)],
+               "ms_per_reduce_scatter": round(wall * 1e3, 3), "algbw_gibs": round(payload / wall / GIB, 2),
+               "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2)}
+        if same is not None:
+            res["int32_equal_to_default"] = sum_over_ranks(1.0 if same else 0.0, world) == world
+        del ref
+        return res
     finally:
         if h1.value:
             lib.pg_close(h1)
@@ -613,11 +621,13 @@ def ring_leg(lib, args, rank, world, transport, sink):
             progress(rank, f"  {transport}: link probe")
             res["link_probe"] = _link_probe(lib, h, rank, world)
         if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
-            progress(rank, f"  {transport}: one-ring comparison")
-            try:
-                res["one_ring"] = _one_ring(lib, rank, world, x, out, count, dt)
-            except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
-                res["one_ring"] = {"error": f"{type(e).__name__}: {e}"}
+            variants = [("one_ring", 1, 6)] + ([("four_rings", 4, 8)] if world >= 5 else [])
+            for key, nr, port_off in variants:
+                progress(rank, f"  {transport}: {nr}-ring comparison")
+                try:
+                    res[key] = _ring_variant(lib, rank, world, x, out, count, dt, nr, port_off)
+                except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
+                    res[key] = {"error": f"{type(e).__name__}: {e}"}
         if os.environ.get("PG_BENCH_ONE_GPU") == "1":
             res["rccl_native"] = "skipped: ranks share one GPU (RCCL refuses duplicate devices)"
         else:

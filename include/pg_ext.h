@@ -39,17 +39,20 @@ extern "C" {
  * reference's chunk_offsets() clamping (src/pg.c:126-138).  Elements. */
 PG_API int pg_block_range(int count, int world, int block, size_t *off, size_t *len);
 
-/* Rings.  With rings = 2 every block is split in two parts that travel in
- * opposite directions, so both directions of each ring link carry data:
- *   part 0 = [0, ceil(len/2)): clockwise (send to rank+1, receive from rank-1),
- *            folded x[b+1] op x[b+2] op ... op x[b]   (indices mod world)
- *   part 1 = [ceil(len/2), len): counter-clockwise (send to rank-1, receive
- *            from rank+1), folded x[b-1] op x[b-2] op ... op x[b]
- * rings = 1: one part, the whole block, clockwise.  Every transport (ring,
- * eager one-shot, xgmi) folds each part in its ring's order, so all of them
- * give identical bits for a given `rings` (PG_RINGS, default 2).  Elements. */
-#define PG_MAX_RINGS 2
+/* Rings.  Every block is split into `rings` parts, part g =
+ * [ceil(g*len/R), ceil((g+1)*len/R)) (part 0 the largest), and part g travels
+ * its own ring of step d = pg_ring_offset(world, rings, g): send to rank+d,
+ * receive from rank-d, folded
+ *     x[b+d] op x[b+2d] op ... op x[b+(W-1)d] op x[b]      (indices mod W)
+ * Steps: +1, -1 (rings = 2, the default: both directions of each ring link
+ * carry data), then +3, -3 (rings = 3, 4: rings over further xGMI links) when
+ * coprime with the world size and new mod world; when those run out the list
+ * repeats.  rings = 1: one part, the whole block, clockwise.  Every transport
+ * (ring, eager one-shot, xgmi) folds each part in its ring's order, so all of
+ * them give identical bits for a given `rings` (PG_RINGS).  Elements. */
+#define PG_MAX_RINGS 4
 PG_API int pg_block_part(size_t len, int rings, int part, size_t *off, size_t *plen);
+PG_API int pg_ring_offset(int world, int rings, int part);
 
 /* Buffer roles named by plan steps. */
 #define PG_BUF_NONE   0
@@ -60,8 +63,8 @@ PG_API int pg_block_part(size_t len, int rings, int part, size_t *off, size_t *p
 
 /* One ring step: in one transport group, send `send_bytes` to rank
  * (rank + send_peer) and receive `recv_bytes` from rank (rank + recv_peer),
- * mod world (+1 / -1: the clockwise ring sends right and receives from the
- * left, the counter-clockwise ring the opposite); then (on the reduce stream,
+ * mod world (d / -d of the step's ring: the clockwise ring sends right and
+ * receives from the left, the counter-clockwise ring the opposite); then (on the reduce stream,
  * after the receive) red_dst[i] = red_dst[i] op red_src[i] for i < red_elems.
  * Offsets/lengths in bytes except red_elems. */
 struct pg_step {
@@ -71,7 +74,7 @@ struct pg_step {
   int32_t send_wait;   /* 1: the sent segment is the previous round's reduce
                           output for `seg`; wait for it before sending        */
   int32_t send_buf, recv_buf, red_dst_buf, red_src_buf;
-  int32_t send_peer, recv_peer; /* rank offsets of the peers: +1 or -1      */
+  int32_t send_peer, recv_peer; /* rank offsets of the peers: d and -d       */
   int64_t send_off, send_bytes;
   int64_t recv_off, recv_bytes;
   int64_t red_dst_off, red_src_off, red_elems;
@@ -80,12 +83,14 @@ struct pg_step {
 /* Reduce-scatter plan for one rank.  Clockwise ring: round k sends block
  * (rank-1-k) and receives block (rank-2-k) mod world -- the reference's
  * rs_send/recv_chunk_index (src/pg.c:141-148) evaluated at rank-1, so that
- * rank r finishes with block r.  Counter-clockwise ring (rings = 2): round k
- * sends block (rank+1+k) and receives block (rank+2+k), its part 1 only.
+ * rank r finishes with block r.  Ring g of step d: round k sends block
+ * (rank-(k+1)d) and receives block (rank-(k+2)d), its part g only (d = -1,
+ * the counter-clockwise ring: blocks rank+1+k and rank+2+k).
  * Segments: chunk_elems_from_bytes(chunk_bytes) (src/pg.c:118-123) elements;
  * parts <= eager_max bytes are one segment; each batch carries `inflight`
- * segment indices of every ring (clockwise steps first).  Ring 1 stages its
- * parts at element ceil(B/2) of the staging blocks (B = ceil(count/world)).
+ * segment indices of every ring (ring 0's steps first).  Ring g stages its
+ * parts at element g*ceil(B/R) of the staging blocks (B = ceil(count/world);
+ * staging blocks hold R*ceil(B/R) elements).
  * out_aliases_src: OUT is block `rank` of SRC (in-place all-reduce).  Returns
  * the number of steps written (or needed, when steps == NULL), -1 on bad
  * arguments. */
@@ -94,9 +99,9 @@ PG_API int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
                            int out_aliases_src, struct pg_step *steps, int max_steps);
 
 /* All-gather plan: round k sends block (rank-k) and receives block
- * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole parts, no reduce; with
- * rings = 2 part 1 of each block goes the other way (round k sends block
- * rank+k to rank-1 and receives block rank+k+1 from rank+1).
+ * (rank-k-1) of OUT (src/pg.c:309-318 indices), whole parts, no reduce; part
+ * g of each block rides ring g of step d (round k sends block rank-k*d to
+ * rank+d and receives block rank-(k+1)*d from rank-d).
  * uniform = 1: blocks of `count` elements (pg_all_gather);
  * uniform = 0: the reduce-scatter partition of `count` (pg_all_reduce). */
 PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform, int rings,
@@ -109,8 +114,8 @@ PG_API int pg_connect_local(int rank, int world, int transport, void **out_handl
 
 /* Run one collective over `world` virtual ranks in this process (transport
  * THREADS): rank r uses sendbufs[r] / recvbufs[r] (HIP device or host
- * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce.  rings: 1 or
- * 2, 0 = PG_RINGS / the default. */
+ * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce.  rings:
+ * 1 .. PG_MAX_RINGS, 0 = PG_RINGS / the default. */
 #define PG_COLL_REDUCE_SCATTER 0
 #define PG_COLL_ALL_GATHER     1
 #define PG_COLL_ALL_REDUCE     2

@@ -57,9 +57,10 @@ PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]
  * (k = nsrc; requires ceil(n / block_elems) <= k): block b folded in exactly
- * the order the ring reduce-scatter uses for it.  rings = 2: the second part
- * of each block (position >= ceil(len_b/2), include/pg_ext.h) is folded
- * srcs[(b-1)%k] op srcs[(b-2)%k] op ... op srcs[b] instead. */
+ * the order the ring reduce-scatter uses for it.  rings = R (1 .. 4): part g
+ * of each block ([ceil(g*len_b/R), ceil((g+1)*len_b/R)), include/pg_ext.h) is
+ * folded srcs[(b+d)%k] op srcs[(b+2d)%k] op ... op srcs[b] with d the step of
+ * ring g (+1, -1, +3, -3 as pg_ring_offset gives them for world = k). */
 PG_API int pgk_fold_blocks(void *out, const void *const *srcs, int nsrc, size_t n, size_t block_elems,
                            int rings, int dt, int op, void *stream);
 

@@ -137,23 +137,43 @@ void orc_ring_block(size_t count, int world, int b, size_t *off_elems, size_t *l
     *len_elems = last - first;
 }
 
+/* Step of ring g of `rings` over `world` ranks (include/pg_ext.h "Rings"):
+ * +1, -1, then +3, -3, +5, ... kept when coprime with world and not yet used
+ * mod world; when they run out the list repeats. */
+int orc_ring_step(int world, int rings, int g) {
+    int offs[4] = {1, -1}, m = 2;
+    for (int c = 3; m < 4 && c < 2 * world; c += 2) {
+        for (int sgn = 1; sgn >= -1 && m < 4; sgn -= 2) {
+            int d = sgn * c, rd = ((d % world) + world) % world, a = rd, b = world;
+            while (b) { int t = a % b; a = b; b = t; }          /* a = gcd(rd, world) */
+            if (rd == 0 || a != 1) continue;
+            int dup = 0;
+            for (int i = 0; i < m; ++i) dup |= ((offs[i] % world) + world) % world == rd;
+            if (!dup) offs[m++] = d;
+        }
+    }
+    (void)rings;
+    return offs[g % m];
+}
+
 int orc_ring_reduce_scatter(int world, void *const *sends, void *const *outs,
                             int count, int dt, int op, int rings) {
     size_t es = orc_elem_size(dt);
-    if (world < 1 || count < 0 || es == 0 || rings < 1 || rings > 2) return -1;
+    if (world < 1 || count < 0 || es == 0 || rings < 1 || rings > 4) return -1;
     for (int b = 0; b < world; ++b) {
         size_t off, len;
         orc_ring_block((size_t)count, world, b, &off, &len);
         if (!len) continue;
-        /* part 0 = [0, h): clockwise ring, acc = x[b+1]; acc = acc op x[b+j], j = 2 .. W
-         * part 1 = [h, len): counter-clockwise ring, x[b-1], x[b-2], ..., x[b]
-         * h = len for one ring, ceil(len/2) for two */
-        size_t h = rings == 1 ? len : (len + 1) / 2;
+        /* part g = [ceil(g*len/R), ceil((g+1)*len/R)) rides the ring of step d:
+         * acc = x[b+d]; acc = acc op x[b+j*d], j = 2 .. W  (x[b+W*d] = x[b]).
+         * One ring: the whole block, d = +1; two: d = +1 then -1. */
         for (int g = 0; g < rings; ++g) {
-            size_t po = g == 0 ? 0 : h, pl = g == 0 ? h : len - h;
+            size_t po = ((size_t)g * len + (size_t)rings - 1) / (size_t)rings;
+            size_t pe = ((size_t)(g + 1) * len + (size_t)rings - 1) / (size_t)rings;
+            size_t pl = pe - po;
             if (!pl) continue;
             char *acc = (char *)outs[b] + po * es;
-            int step = g == 0 ? 1 : world - 1;
+            int step = ((orc_ring_step(world, rings, g) % world) + world) % world;
             memcpy(acc, (const char *)sends[(b + step) % world] + (off + po) * es, pl * es);
             for (int j = 2; j <= world; ++j)
                 orc_reduce_inplace(acc, (const char *)sends[(b + j * step) % world] + (off + po) * es, pl, dt, op);

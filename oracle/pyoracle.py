@@ -54,6 +54,7 @@ class Oracle:
             "orc_mock_all_gather": (_I, [_I, _I, _VP, _VP, _I, _I]),
             "orc_mock_all_reduce": (_I, [_I, _I, _SZ, _VP, _VP, _I, _I, _I]),
             "orc_ring_reduce_scatter": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _I]),
+            "orc_ring_step": (_I, [_I, _I, _I]),
             "orc_ring_all_gather": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I]),
             "orc_ring_all_reduce": (_I, [_I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _I]),
             "orc_ring_block": (None, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
@@ -92,12 +93,16 @@ class Oracle:
         return rc, r
 
     # -- real-ring semantics ----------------------------------------------------------
+    def ring_step(self, world, rings, g):
+        return self.lib.orc_ring_step(world, rings, g)
+
     def ring_block(self, count, world, b):
         off, ln = _SZ(), _SZ()
         self.lib.orc_ring_block(count, world, b, ctypes.byref(off), ctypes.byref(ln))
         return off.value, ln.value
 
-    # rings: 2 = the library default (PG_RINGS), 1 = one clockwise ring (include/pg_ext.h)
+    # rings: 2 = the library default (PG_RINGS), 1 = one clockwise ring, 3 / 4 = rings of
+    # step +3 / -3 added (include/pg_ext.h)
     def ring_reduce_scatter(self, sends, dt, op, rings=2):
         world, count = len(sends), sends[0].size
         outs = [np.zeros(self.ring_block(count, world, b)[1], dtype=NP_DTYPE[dt]) for b in range(world)]

@@ -152,6 +152,9 @@ static void *copy_thread(void *arg) {
   struct copy_job *j = (struct copy_job *)arg;
   j->err = hipSetDevice(j->device);
   if (j->err == hipSuccess) j->err = hipMemcpy(j->dst, j->src, j->bytes, hipMemcpyDefault);
+  /* a host-to-device hipMemcpy may return once the bytes are staged, before
+   * they land; the consumers run on non-blocking streams, so wait for them */
+  if (j->err == hipSuccess) j->err = hipStreamSynchronize(NULL);
   return NULL;
 }
 
@@ -165,6 +168,7 @@ int pg_copy_parallel(void *dst, const void *src, size_t bytes) {
   }
   if (nthreads == 1 || bytes < (32u << 20)) {
     PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    PG_CHECK_HIP(hipStreamSynchronize(NULL));                 /* as in copy_thread */
     return 0;
   }
   int dev = 0;
@@ -196,7 +200,11 @@ static int copy_any(void *dst, const void *src, size_t bytes) {
   int dd = pg_is_device_ptr(dst), sd = pg_is_device_ptr(src);
   if (!dd && !sd) { memmove(dst, src, bytes); return 0; }
   if (dd != sd) return pg_copy_parallel(dst, src, bytes);      /* crosses PCIe */
-  PG_CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  /* device to device: hipMemcpy may return before the copy has landed, and
+   * the comm / reduce streams are non-blocking (no implicit wait on the null
+   * stream), so a send enqueued next could read the old bytes: wait here */
+  PG_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, NULL));
+  PG_CHECK_HIP(hipStreamSynchronize(NULL));
   return 0;
 }
 
@@ -228,7 +236,7 @@ int pg_impl_create(struct pg *pg) {
   e = getenv("PG_RINGS");
   if (e && *e) {
     im->rings = atoi(e);
-    if (im->rings < 1 || im->rings > PG_MAX_RINGS) { pg_set_error("PG_RINGS=%s: expected 1 or 2", e); return -1; }
+    if (im->rings < 1 || im->rings > PG_MAX_RINGS) { pg_set_error("PG_RINGS=%s: expected 1 .. %d", e, PG_MAX_RINGS); return -1; }
   }
   return 0;
 }
@@ -367,7 +375,8 @@ static int plan_into(struct pg_impl *im, int is_rs, int count, int dt, int alias
 
 static int ensure_stage(struct pg_impl *im, int count, int dt) {
   size_t blk = ((size_t)count + (size_t)im->pg->world_size - 1) / (size_t)im->pg->world_size;
-  size_t bytes = blk * pg_elem_size(dt);
+  size_t R = (size_t)im->rings, part = (blk + R - 1) / R;        /* ring g stages at g*part (pg_plan.c) */
+  size_t bytes = R * part * pg_elem_size(dt);
   size_t cap1 = im->stage_cap;
   if (pg_ensure(&im->stage[0], &im->stage_cap, bytes)) return -1;
   return pg_ensure(&im->stage[1], &cap1, bytes);
@@ -406,14 +415,14 @@ static int upload_block(struct pg *pg, struct stage_ctx *c, int b) {
   return len ? pg_timed_copy(c->dev_src + off * es, c->host_src + off * es, len * es, c->h2d_us) : 0;
 }
 
-/* reduce-scatter rounds: round k reads source blocks r-1 (k = 0, sent) and
- * r-2-k; the counter-clockwise ring (rings = 2) reads r+1 and r+2+k */
+/* reduce-scatter rounds: ring g of step d reads source blocks r-d (k = 0,
+ * sent) and r-(2+k)d in round k (d = +1: r-1 and r-2-k) */
 static int rs_upload_hook(struct pg_impl *im, void *ctx, int k) {
   struct pg *pg = im->pg;
   struct stage_ctx *c = (struct stage_ctx *)ctx;
   if (k >= pg->world_size - 1) return 0;
   for (int g = 0; g < im->rings; ++g) {
-    const int d = g == 0 ? -1 : 1;                                /* direction of the block walk */
+    const int d = -pg_ring_offset(pg->world_size, im->rings, g);   /* step of the block walk */
     if (k == 0 && upload_block(pg, c, pg->rank + d)) return -1;
     if (upload_block(pg, c, pg->rank + d * (2 + k))) return -1;
     if (k == 0 && upload_block(pg, c, pg->rank + d * 3)) return -1;   /* one block of lead */
@@ -421,9 +430,9 @@ static int rs_upload_hook(struct pg_impl *im, void *ctx, int k) {
   return 0;
 }
 
-/* all-gather rounds: the clockwise ring receives block r-j-1 in round j, the
- * counter-clockwise one (rings = 2) block r+j+1, so block b is complete after
- * round max((r-1-b) mod W, (b-r-1) mod W).  Before round k starts, every
+/* all-gather rounds: ring g of step d receives block r-(j+1)d in round j, so
+ * block b is complete after the latest of those rounds over the rings
+ * (d = +1: (r-1-b) mod W; d = -1: (b-r-1) mod W).  Before round k starts, every
  * round < k has been enqueued; wait for the last recorded one (stream order
  * covers the earlier ones) and download the blocks completed in rounds
  * next_dl .. k-1.  Called with k = world-1 after the last round.  Empty
@@ -437,10 +446,11 @@ static int ag_download_hook(struct pg_impl *im, void *ctx, int k) {
   size_t es = pg_elem_size(c->dt);
   for (int b = 0; b < W; ++b) {
     if (b == r) continue;
-    int done = ((r - 1 - b) % W + W) % W;
-    if (im->rings == 2) {
-      int j1 = ((b - r - 1) % W + W) % W;
-      if (j1 > done) done = j1;
+    int done = 0;
+    for (int g = 0; g < im->rings; ++g) {
+      const int d = pg_ring_offset(W, im->rings, g);
+      for (int j = 0; j + 1 < W; ++j)
+        if ((((r - (j + 1) * d) % W) + W) % W == b) { if (j > done) done = j; break; }
     }
     if (done < c->next_dl || done >= k) continue;
     size_t off, len;

@@ -14,8 +14,8 @@
  *   all-reduce      every rank sends its whole input to every peer and
  *                   pgk_fold_blocks folds each block in its ring order.
  *
- * Fold order = the ring's (block b: x[b+1] op x[b+2] op ... op x[b]; with two
- * rings the second part of each block x[b-1] op x[b-2] op ... op x[b]; see
+ * Fold order = the ring's (part g of block b: x[b+d] op x[b+2d] op ... op x[b]
+ * with d = pg_ring_offset(W, rings, g): +1, -1, +3, -3; see
  * pg_plan.c, include/pg_ext.h and DESIGN.md §2), so results are bit-identical
  * to the ring path for int32 and double alike.  Used by the point-to-point transports (RCCL,
  * in-process threads) for W <= 16; xgmi has its own direct-read one-shot.
@@ -86,8 +86,9 @@ int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int cou
     pg_block_part(blen, im->rings, g, &po, &pl);
     if (!pl) continue;
     const void *srcs[EAGER_MAX_WORLD];
+    const int d = pg_ring_offset(W, im->rings, g);
     for (int j = 0; j < W; ++j) {
-      int q = g == 0 ? (r + 1 + j) % W : ((r - 1 - j) % W + W) % W;   /* the part's ring order */
+      int q = ((r + (j + 1) * d) % W + W) % W;                        /* the part's ring order */
       const char *base = q == r ? src + boff * es : gat + (size_t)q * slot;
       srcs[j] = base + po * es;
     }

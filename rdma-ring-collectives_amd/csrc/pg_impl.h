@@ -70,7 +70,7 @@ struct pg_impl {
   void *dout;      size_t dout_cap;   /* device result / full buffer          */
   void *ebuf;      size_t ebuf_cap;   /* eager one-shot gather area (pg_eager.c) */
   int eager_oneshot;          /* PG_EAGER_ONESHOT, default 1                  */
-  int rings;                  /* PG_RINGS: 1 or 2 (default), pg_ext.h          */
+  int rings;                  /* PG_RINGS: 1 .. 4, default 2, pg_ext.h         */
 
   struct pg_step *steps; int steps_cap;
   int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */

@@ -19,8 +19,10 @@
  *     src/pg.c:282-287);
  *   - with rings = 2 (default) the second half of every block runs the mirror
  *     schedule in the other direction, so both directions of each link carry
- *     data (SURVEY.md §8f "bidirectional ring"); the reference's README
- *     describes one ring (README.md:68-71).
+ *     data (SURVEY.md §8f "bidirectional ring"); rings = 3, 4 add rings of
+ *     step +3 / -3 (world permitting: pg_ring_offset), each over its own pair
+ *     of xGMI links (§8f "multi-ring"); the reference's README describes one
+ *     ring (README.md:68-71).
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -60,10 +62,36 @@ static size_t nsegs(size_t len, size_t seg) { return len ? (len + seg - 1) / seg
 
 int pg_block_part(size_t len, int rings, int part, size_t *off, size_t *plen) {
   if (rings < 1 || rings > PG_MAX_RINGS || part < 0 || part >= rings || !off || !plen) return -1;
-  size_t h = rings == 1 ? len : (len + 1) / 2;
-  *off = part == 0 ? 0 : h;
-  *plen = part == 0 ? h : len - h;
+  /* part g = [ceil(g*len/R), ceil((g+1)*len/R)): part 0 is the largest */
+  size_t a = ((size_t)part * len + (size_t)rings - 1) / (size_t)rings;
+  size_t b = ((size_t)(part + 1) * len + (size_t)rings - 1) / (size_t)rings;
+  *off = a;
+  *plen = b - a;
   return 0;
+}
+
+static int gcd_int(int a, int b) {
+  while (b) { int t = a % b; a = b; b = t; }
+  return a;
+}
+
+int pg_ring_offset(int world, int rings, int part) {
+  if (world < 1 || rings < 1 || rings > PG_MAX_RINGS || part < 0 || part >= rings) return 0;
+  /* +1 and -1 (the bidirectional pair, also at world 2 where they coincide),
+   * then +3, -3, +5, -5, ... kept when coprime with world and not already
+   * used mod world; when those run out the list repeats (more segment streams
+   * over the same links) */
+  int offs[PG_MAX_RINGS] = {1, -1}, m = 2;
+  for (int c = 3; m < PG_MAX_RINGS && c < 2 * world; c += 2) {
+    for (int sgn = 1; sgn >= -1 && m < PG_MAX_RINGS; sgn -= 2) {
+      int d = sgn * c, rd = ring_mod(d, world);
+      if (rd == 0 || gcd_int(rd, world) != 1) continue;
+      int dup = 0;
+      for (int i = 0; i < m; ++i) dup |= ring_mod(offs[i], world) == rd;
+      if (!dup) offs[m++] = d;
+    }
+  }
+  return offs[part % m];
 }
 
 static void put(struct pg_step *steps, int max_steps, int n, const struct pg_step *s) {
@@ -73,7 +101,7 @@ static void put(struct pg_step *steps, int max_steps, int n, const struct pg_ste
 /* One ring's view of round k: the blocks it sends and receives (this rank's
  * parts of them) and how they are cut into segments. */
 struct ring_round {
-  int dir;                      /* +1 clockwise, -1 counter-clockwise       */
+  int d;                        /* ring offset: send to rank+d, receive from rank-d */
   size_t so, sl, to, tl;        /* sent / received block: offset, length    */
   size_t sp, spl, tp, tpl;      /* this ring's part of each: offset, length */
   size_t sseg, tseg, ns, nt;    /* segment lengths and counts               */
@@ -98,10 +126,11 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
     size_t nj = 0;
     for (int g = 0; g < rings; ++g) {
       struct ring_round *q = &rr[g];
-      q->dir = g == 0 ? 1 : -1;
-      /* clockwise: rs_send/recv_chunk_index(k, rank-1); counter-clockwise: the mirror */
-      int sb = g == 0 ? ring_mod(rank - 1 - k, world) : ring_mod(rank + 1 + k, world);
-      int tb = g == 0 ? ring_mod(rank - 2 - k, world) : ring_mod(rank + 2 + k, world);
+      q->d = pg_ring_offset(world, rings, g);
+      /* d = +1: rs_send/recv_chunk_index(k, rank-1); other rings: the same walk
+       * with step d (d = -1: the mirror, counter-clockwise ring) */
+      int sb = ring_mod(rank - (k + 1) * q->d, world);
+      int tb = ring_mod(rank - (k + 2) * q->d, world);
       pg_block_range(count, world, sb, &q->so, &q->sl);
       pg_block_range(count, world, tb, &q->to, &q->tl);
       pg_block_part(q->sl, rings, g, &q->sp, &q->spl);
@@ -110,7 +139,7 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
       q->tseg = seg_elems_for(q->tpl, es, chunk_bytes, eager_max);
       q->ns = nsegs(q->spl, q->sseg);
       q->nt = nsegs(q->tpl, q->tseg);
-      q->stage_base = g == 0 ? 0 : (bfull + 1) / 2;
+      q->stage_base = (size_t)g * ((bfull + (size_t)rings - 1) / (size_t)rings);   /* parts <= ceil(B/R) */
       q->seg_base = g * seg_stride;
       size_t m = q->ns > q->nt ? q->ns : q->nt;
       if (m > nj) nj = m;
@@ -128,8 +157,8 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
           st.round = k;
           st.batch = batch;
           st.seg = q->seg_base + (int32_t)j;
-          st.send_peer = q->dir;
-          st.recv_peer = -q->dir;
+          st.send_peer = q->d;
+          st.recv_peer = -q->d;
           if (j < q->ns) {
             size_t e0 = j * q->sseg, len = q->spl - e0 < q->sseg ? q->spl - e0 : q->sseg;
             if (k == 0) { st.send_buf = PG_BUF_SRC; st.send_off = (int64_t)((q->so + q->sp + e0) * es); }
@@ -182,8 +211,9 @@ int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform
   int n = 0;
   for (int k = 0; k + 1 < world; ++k) {
     for (int g = 0; g < rings; ++g) {
-      int sb = g == 0 ? ring_mod(rank - k, world) : ring_mod(rank + k, world);          /* src/pg.c:310 */
-      int rb = g == 0 ? ring_mod(rank - k - 1, world) : ring_mod(rank + k + 1, world);  /* src/pg.c:311 */
+      const int d = pg_ring_offset(world, rings, g);
+      int sb = ring_mod(rank - k * d, world);          /* d = +1: src/pg.c:310 */
+      int rb = ring_mod(rank - (k + 1) * d, world);    /* d = +1: src/pg.c:311 */
       size_t so, sl, ro, rl, sp, spl, rp, rpl;
       if (uniform) { so = (size_t)sb * (size_t)count; sl = (size_t)count; ro = (size_t)rb * (size_t)count; rl = (size_t)count; }
       else { pg_block_range(count, world, sb, &so, &sl); pg_block_range(count, world, rb, &ro, &rl); }
@@ -195,8 +225,8 @@ int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform
       st.round = k;
       st.batch = k;
       st.seg = g;
-      st.send_peer = g == 0 ? 1 : -1;
-      st.recv_peer = -st.send_peer;
+      st.send_peer = d;
+      st.recv_peer = -d;
       if (spl) { st.send_buf = PG_BUF_OUT; st.send_off = (int64_t)((so + sp) * es); st.send_bytes = (int64_t)(spl * es); }
       if (rpl) { st.recv_buf = PG_BUF_OUT; st.recv_off = (int64_t)((ro + rp) * es); st.recv_bytes = (int64_t)(rpl * es); }
       put(steps, max_steps, n, &st);

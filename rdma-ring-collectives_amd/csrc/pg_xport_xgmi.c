@@ -543,8 +543,9 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
     pg_block_part(len, im->rings, g, &po, &pl);
     if (!pl) continue;
     const void *srcs[16];
+    const int d = pg_ring_offset(W, im->rings, g);
     for (int j = 0; j < W; ++j) {
-      int q = g == 0 ? (r + 1 + j) % W : ((r - 1 - j) % W + W) % W;
+      int q = ((r + (j + 1) * d) % W + W) % W;
       srcs[j] = by_rank[q] + (off_elems + po) * es;
       pg_trace(pg, "xgmi fold: part %d source %d = rank %d at %p", g, j, q, srcs[j]);
     }

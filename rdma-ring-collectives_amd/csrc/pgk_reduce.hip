@@ -180,21 +180,29 @@ __global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_scalar(T* __restri
 }
 
 // One-shot all-reduce fold: element i belongs to ring block b = i / block_elems
-// and is folded in that block's ring order, src[(b+1)%k] op src[(b+2)%k] ...
-// op src[b] -- the order the reduce-scatter uses for block b, so every rank
-// computing the whole vector this way gets the all-reduce result bit for bit.
-// With two rings the second part of a block (position >= ceil(len_b / 2))
-// travels the other way and folds src[(b-1)%k] op src[(b-2)%k] ... op src[b].
-// Used for small messages, where one launch beats reduce-scatter + gather.
+// and is folded in that block's ring order -- the order the reduce-scatter
+// uses for it -- so every rank computing the whole vector this way gets the
+// all-reduce result bit for bit.  Block b (length len) is cut into `rings`
+// parts, part g = [ceil(g*len/R), ceil((g+1)*len/R)), and part g travels the
+// ring of step d_g (include/pg_ext.h): src[(b+d)%k] op src[(b+2d)%k] ... op
+// src[b].  steps[g] = d_g mod k.  Used for small messages, where one launch
+// beats reduce-scatter + gather.
+constexpr int kMaxRings = 4;
+struct RingSteps {
+  int d[kMaxRings];
+};
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kMultiBlock) void k_fold_blocks(T* __restrict__ out, SrcList<T> src, int k,
-                                                             size_t n, size_t block_elems, int rings) {
+                                                             size_t n, size_t block_elems, int rings,
+                                                             RingSteps steps) {
   const size_t stride = (size_t)gridDim.x * kMultiBlock;
   for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < n; i += stride) {
     const int b = (int)(i / block_elems);
     const size_t b0 = (size_t)b * block_elems;
     const size_t len = n - b0 < block_elems ? n - b0 : block_elems;
-    const int step = (rings == 2 && i - b0 >= (len + 1) / 2) ? k - 1 : 1;   // -1 mod k
+    const int g = (int)((i - b0) * (size_t)rings / len);     // ceil(g*len/R) <= p  <=>  g <= p*R/len
+    const int step = steps.d[g];
     int q = b + step >= k ? b + step - k : b + step;
     T acc = src.p[q][i];
     for (int j = 1; j < k; ++j) {
@@ -449,12 +457,32 @@ int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int
 }
 
 
+// Step of ring `part` among `rings` over `world` ranks: +1, -1, then +3, -3,
+// ... kept when coprime with world and new mod world, repeating when they run
+// out.  The same rule as pg_ring_offset (pg_plan.c); the kernel library keeps
+// its own copy so that include/pgk.h stands alone.
+static int ring_step(int world, int rings, int part) {
+  int offs[kMaxRings] = {1, -1}, m = 2;
+  auto mod = [world](int x) { return ((x % world) + world) % world; };
+  auto gcd = [](int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; };
+  for (int c = 3; m < kMaxRings && c < 2 * world; c += 2)
+    for (int sgn = 1; sgn >= -1 && m < kMaxRings; sgn -= 2) {
+      int d = sgn * c, rd = mod(d);
+      if (rd == 0 || gcd(rd, world) != 1) continue;
+      bool dup = false;
+      for (int i = 0; i < m; ++i) dup |= mod(offs[i]) == rd;
+      if (!dup) offs[m++] = d;
+    }
+  (void)rings;
+  return offs[part % m];
+}
+
 int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size_t block_elems, int rings,
                     int dt, int op, void* stream) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
-  if (rings != 1 && rings != 2) { set_err("pgk: rings %d, expected 1 or 2", rings); return -1; }
+  if (rings < 1 || rings > kMaxRings) { set_err("pgk: rings %d, expected 1 .. %d", rings, kMaxRings); return -1; }
   if (n == 0) return 0;
   if (!out || !srcs || block_elems == 0 || (n + block_elems - 1) / block_elems > (size_t)nsrc) {
     set_err("pgk: bad fold_blocks arguments");
@@ -463,24 +491,26 @@ int pgk_fold_blocks(void* out, const void* const* srcs, int nsrc, size_t n, size
   size_t g = (n + kMultiBlock - 1) / kMultiBlock;
   if (g > 65536) g = 65536;
   hipStream_t s = (hipStream_t)stream;
+  RingSteps rs{};
+  for (int p = 0; p < rings; ++p) rs.d[p] = ((ring_step(nsrc, rings, p) % nsrc) + nsrc) % nsrc;
   if (dt == PGK_DT_INT32) {
     SrcList<uint32_t> sl{};
     for (int j = 0; j < nsrc; ++j) sl.p[j] = (const uint32_t*)srcs[j];
     if (op == PGK_OP_SUM)
       hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (uint32_t*)out, sl, nsrc, n, block_elems, rings);
+                         (uint32_t*)out, sl, nsrc, n, block_elems, rings, rs);
     else
       hipLaunchKernelGGL((k_fold_blocks<uint32_t, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (uint32_t*)out, sl, nsrc, n, block_elems, rings);
+                         (uint32_t*)out, sl, nsrc, n, block_elems, rings, rs);
   } else {
     SrcList<double> sl{};
     for (int j = 0; j < nsrc; ++j) sl.p[j] = (const double*)srcs[j];
     if (op == PGK_OP_SUM)
       hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_SUM>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (double*)out, sl, nsrc, n, block_elems, rings);
+                         (double*)out, sl, nsrc, n, block_elems, rings, rs);
     else
       hipLaunchKernelGGL((k_fold_blocks<double, PGK_OP_PROD>), dim3((unsigned)g), dim3(kMultiBlock), 0, s,
-                         (double*)out, sl, nsrc, n, block_elems, rings);
+                         (double*)out, sl, nsrc, n, block_elems, rings, rs);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }

@@ -85,6 +85,7 @@ _SIGS = {
     "pg_plan_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _SZ, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_block_part": (_I, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "pg_ring_offset": (_I, [_I, _I, _I]),
     "pgx_xgmi_link_probe": (_I, [_VP, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
     "pg_connect_local": (_I, [_I, _I, _I, ctypes.POINTER(_VP)]),
     "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I, _I]),
@@ -160,6 +161,11 @@ def block_part(length: int, rings: int, part: int) -> tuple[int, int]:
     off, ln = ctypes.c_size_t(), ctypes.c_size_t()
     check(lib.pg_block_part(length, rings, part, ctypes.byref(off), ctypes.byref(ln)), "pg_block_part")
     return off.value, ln.value
+
+
+def ring_offset(world: int, rings: int, part: int) -> int:
+    """Step d of ring `part` (send to rank+d, receive from rank-d; include/pg_ext.h)."""
+    return load().pg_ring_offset(world, rings, part)
 
 
 def plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max=4096, inflight=4, alias=0, rings=2):

@@ -100,7 +100,8 @@ def run_plans(plans, bufs_per_rank, dt, op):
 def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False, rings=2):
     world, count = len(sends), sends[0].size
     es = 4 if dt == 0 else 8
-    bmax = -(-count // world) * es if count else 0
+    blk = -(-count // world) if count else 0
+    bmax = rings * -(-blk // rings) * es          # staging block: R * ceil(B/R) elements (include/pg_ext.h)
     plans, bufs = [], []
     for r in range(world):
         plans.append(pgamd.plan_reduce_scatter(r, world, count, dt, chunk_bytes, eager_max, inflight, int(alias),

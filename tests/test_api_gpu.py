@@ -204,7 +204,7 @@ CASES = [  # world, dt, op, count, chunk_bytes, eager_max, inflight
 ]
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
 @pytest.mark.parametrize("case", CASES)
 def test_ring_reduce_scatter_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count, cb, eager, infl = case
@@ -217,7 +217,7 @@ def test_ring_reduce_scatter_sim(gpu, lib, oracle, case, rings):
             assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (case, r, on_dev)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 4])
 @pytest.mark.parametrize("case", CASES)
 def test_ring_all_reduce_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count, cb, eager, infl = case
@@ -238,7 +238,7 @@ def test_ring_all_reduce_sim(gpu, lib, oracle, case, rings):
             assert got[r].tobytes() == want[r].tobytes(), (case, r, on_dev, in_place)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
 @pytest.mark.parametrize("world,count", [(2, 1), (3, 1000), (4, 0), (8, 4099)])
 def test_ring_all_gather_sim(gpu, lib, oracle, world, count, rings):
     for dt in (0, 1):
@@ -274,7 +274,7 @@ EAGER_CASES = [  # world, dt, op, count   (eager_max = 4096 bytes)
 ]
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 4])
 @pytest.mark.parametrize("case", EAGER_CASES)
 def test_eager_oneshot_sim(gpu, lib, oracle, case, rings):
     world, dt, op, count = case
@@ -305,7 +305,7 @@ def test_eager_oneshot_sim(gpu, lib, oracle, case, rings):
             assert got[r].tobytes() == want_ag[r].tobytes(), (case, "ag", r, on_dev)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 4])
 def test_eager_matches_ring_bytes(gpu, lib, oracle, monkeypatch, rings):
     """Same inputs through the one-shot and through the W-1 round ring
     (PG_EAGER_ONESHOT=0): byte-identical outputs, doubles included."""

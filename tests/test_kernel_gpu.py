@@ -228,7 +228,7 @@ def test_fold_blocks_and_gather(gpu, lib, oracle):
     import ctypes
     torch = gpu
     cases = ((2, 1001, 1, 0), (3, 10, 0, 1), (8, 65541, 1, 1), (5, 4, 1, 0), (4, 4099, 0, 0), (7, 7001, 1, 0))
-    for (world, count, dt, op), rings in itertools.product(cases, (1, 2)):
+    for (world, count, dt, op), rings in itertools.product(cases, (1, 2, 3, 4)):
         xs = [oracle.fill(count, dt, op, 77 + r) for r in range(world)]
         want = oracle.ring_all_reduce(xs, dt, op, rings)[0]
         D = [to_dev(torch, x) for x in xs]
@@ -237,7 +237,7 @@ def test_fold_blocks_and_gather(gpu, lib, oracle):
         blk = -(-count // world)
         assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, rings, dt, op, stream(torch)) == 0
         assert to_host(torch, out).tobytes() == want.tobytes(), (world, count, dt, op, rings)
-    assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, 3, 1, 0, stream(torch)) == -1
+    assert lib.pgk_fold_blocks(ptr(out), srcs, world, count, blk, 5, 1, 0, stream(torch)) == -1
     # gather: ranges of different sizes/alignments into one buffer
     src = torch.arange(1 << 16, dtype=torch.int32, device="cuda")
     dst = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")

@@ -112,11 +112,12 @@ def test_splitmix_stream(oracle):
     assert np.array_equal(a.view(np.uint32), (z >> np.uint64(32)).astype(np.uint32))
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
 def test_ring_simulator_semantics(oracle, rings):
     """orc_ring_*: integer sums equal the wrapped total; doubles follow the
-    documented fold order x[b+1] op x[b+2] op ... op x[b] (with two rings the
-    second part of each block, from ceil(len/2) on, x[b-1] op ... op x[b])."""
+    documented fold order x[b+1] op x[b+2] op ... op x[b] (with R rings, part
+    g = [ceil(g*len/R), ceil((g+1)*len/R)) of each block x[b+d] op x[b+2d] op
+    ... op x[b], d = +1, -1, +3, -3 where coprime with W and new mod W)."""
     rng = np.random.default_rng(7)
     for world in (1, 2, 3, 5, 8):
         for count in (0, 1, 7, 64, 1001):
@@ -130,10 +131,17 @@ def test_ring_simulator_semantics(oracle, rings):
                 assert np.array_equal(outs[b].view(np.uint32), total[off:off + ln])
             fs = [rng.standard_normal(count) * np.exp2(rng.integers(-30, 31, count)) for _ in range(world)]
             outs = oracle.ring_reduce_scatter(fs, 1, 0, rings)
+            steps, c = [1, -1], 3
+            while len(steps) < 4 and c < 2 * world:
+                for d in (c, -c):
+                    if len(steps) < 4 and d % world and np.gcd(d % world, world) == 1 and \
+                            all(d % world != e % world for e in steps):
+                        steps.append(d)
+                c += 2
             for b in range(world):
                 off, ln = oracle.ring_block(count, world, b)
-                h = ln if rings == 1 else (ln + 1) // 2
-                for lo, hi, step in ((0, h, 1), (h, ln, world - 1)):
+                for g in range(rings):
+                    lo, hi, step = -(-g * ln // rings), -(-(g + 1) * ln // rings), steps[g % len(steps)] % world
                     acc = fs[(b + step) % world][off + lo:off + hi].copy()
                     for j in range(2, world + 1):
                         acc = acc + fs[(b + j * step) % world][off + lo:off + hi]

@@ -28,19 +28,38 @@ def test_plan_rejects_bad_arguments(lib):
     assert lib.pg_plan_reduce_scatter(2, 2, 8, 0, 16, 0, 1, 2, 0, None, 0) == -1
     assert lib.pg_plan_reduce_scatter(0, 2, -1, 0, 16, 0, 1, 2, 0, None, 0) == -1
     assert lib.pg_plan_reduce_scatter(0, 2, 8, 9, 16, 0, 1, 2, 0, None, 0) == -1
-    assert lib.pg_plan_reduce_scatter(0, 2, 8, 0, 16, 0, 1, 3, 0, None, 0) == -1      # rings 1 or 2
+    assert lib.pg_plan_reduce_scatter(0, 2, 8, 0, 16, 0, 1, 5, 0, None, 0) == -1      # rings 1 .. 4
     assert lib.pg_plan_reduce_scatter(0, 2, 8, 0, 16, 0, 1, 0, 0, None, 0) == -1
     assert lib.pg_plan_all_gather(0, 2, 8, 9, 1, 2, None, 0) == -1
-    assert lib.pg_plan_all_gather(0, 2, 8, 0, 1, 3, None, 0) == -1
+    assert lib.pg_plan_all_gather(0, 2, 8, 0, 1, 5, None, 0) == -1
     assert lib.pg_plan_reduce_scatter(0, 1, 8, 0, 16, 0, 1, 2, 0, None, 0) == 0
 
 
 def test_block_parts():
-    for ln in (0, 1, 2, 7, 8, 1001):
+    for ln in (0, 1, 2, 3, 7, 8, 1001):
         assert pgamd.block_part(ln, 1, 0) == (0, ln)
         h = (ln + 1) // 2
         assert pgamd.block_part(ln, 2, 0) == (0, h)
         assert pgamd.block_part(ln, 2, 1) == (h, ln - h)
+        for rings in (3, 4):
+            parts = [pgamd.block_part(ln, rings, g) for g in range(rings)]
+            assert parts[0][0] == 0 and sum(p[1] for p in parts) == ln
+            assert all(a[0] + a[1] == b[0] for a, b in zip(parts, parts[1:]))     # contiguous
+            assert parts[0][1] == -(-ln // rings) and all(p[1] <= parts[0][1] for p in parts)
+
+
+def test_ring_offsets(oracle):
+    # +1, -1, then +3, -3 where coprime with the world and new mod world; else repeat
+    want = {2: [1, -1, 1, -1], 3: [1, -1, 1, -1], 4: [1, -1, 1, -1], 5: [1, -1, 3, -3],
+            6: [1, -1, 1, -1], 7: [1, -1, 3, -3], 8: [1, -1, 3, -3], 9: [1, -1, 5, -5], 16: [1, -1, 3, -3]}
+    for world, offs in want.items():
+        assert [pgamd.ring_offset(world, 4, g) for g in range(4)] == offs, world
+    for world in range(1, 17):
+        for rings in range(1, 5):
+            for g in range(rings):
+                d = pgamd.ring_offset(world, rings, g)
+                assert d == oracle.ring_step(world, rings, g)
+                assert world == 1 or np.gcd(d % world, world) == 1
 
 
 def test_plan_shape():
@@ -79,7 +98,7 @@ def test_plan_shape_two_rings():
     assert all(s["recv_buf"] == pgamd.PG_BUF_OUT for s in st if s["round"] == 2)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 def test_plan_edges_pair_up(world, rings):
     """Per directed edge, the sizes one rank sends equal, in order, the sizes its peer receives."""
@@ -92,8 +111,8 @@ def test_plan_edges_pair_up(world, rings):
                 assert sends == recvs, (world, r, q, count, dt, cb)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
-@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 8])
 def test_plan_reduce_scatter_matches_oracle(oracle, world, rings):
     for dt, op, count, cb, infl in itertools.product((0, 1), (0, 1), (0, 1, 5, 64, 1001), (8, 24, 4096), (1, 4)):
         xs = inputs(oracle, world, count, dt, op, count + world)
@@ -125,8 +144,8 @@ def test_two_rings_fold_order_differs_for_double(oracle):
     assert all(x.tobytes() == y.tobytes() for x, y in zip(ai, bi))
 
 
-@pytest.mark.parametrize("rings", [1, 2])
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("rings", [1, 2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 def test_plan_all_reduce_in_place_matches_oracle(oracle, world, rings):
     for dt, op, count in itertools.product((0, 1), (0, 1), (1, 7, 100, 1001)):
         xs = inputs(oracle, world, count, dt, op, 99 + count)
@@ -136,7 +155,7 @@ def test_plan_all_reduce_in_place_matches_oracle(oracle, world, rings):
             assert got[r].tobytes() == want[r].tobytes(), (world, r, dt, op, count)
 
 
-@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
 def test_plan_all_gather_matches_oracle(oracle, world, rings):
     for dt, count in itertools.product((0, 1), (0, 1, 13, 512)):

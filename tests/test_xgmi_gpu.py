@@ -105,7 +105,7 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2, mode="rea
     (8, 1 << 20, "1", 2, "read"), (2, 0, "1", 2, "read"), (5, 0, "1", 2, "read"), (4, 1 << 40, "1", 2, "read"),
     (3, 1 << 20, "0", 2, "read"), (4, 0, "0", 2, "read"), (4, 1 << 20, "1", 1, "read"), (3, 1 << 40, "0", 1, "read"),
     (2, 1 << 20, "1", 2, "push"), (4, 0, "1", 2, "push"), (8, 1 << 20, "1", 2, "push"), (3, 0, "1", 1, "push"),
-    (5, 0, "0", 2, "push")])
+    (5, 0, "0", 2, "push"), (8, 1 << 20, "1", 4, "read"), (5, 0, "1", 3, "push"), (4, 1 << 40, "1", 4, "read")])
 def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy, rings, mode):
     """oneshot_max selects the all-reduce form: 0 = always reduce-scatter +
     gather, 2^40 = always the one-shot fold, 1 MiB = the default split.
