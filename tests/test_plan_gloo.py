@@ -41,12 +41,13 @@ def _worker(rank, world, port, q):
         fails = []
         for (dt, op, count, cb, infl), rings in itertools.product(
                 ((0, 0, 1000, 64, 2), (1, 0, 4099, 256, 4), (1, 1, 77, 8, 1), (0, 1, 3, 4, 1), (1, 0, 0, 64, 1)),
-                (1, 2)):
+                (1, 2, 4)):
             es = 4 if dt == 0 else 8
             xs = [orc.fill(count, dt, op, 500 + 17 * q_ + count) for q_ in range(world)]
             want = orc.ring_reduce_scatter(xs, dt, op, rings)[rank]
             off, ln = pgamd.block_range(count, world, rank)
-            bmax = -(-count // world) * es if count else 0
+            blk = -(-count // world) if count else 0
+            bmax = rings * -(-blk // rings) * es          # staging: R * ceil(B/R) elements
             bufs = {pgamd.PG_BUF_SRC: xs[rank].copy().view(np.uint8), pgamd.PG_BUF_OUT: np.zeros(ln * es, np.uint8),
                     pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)}
             steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl, rings=rings)
@@ -85,7 +86,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 5])
 def test_ring_plan_over_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
