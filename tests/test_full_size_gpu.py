@@ -1,0 +1,75 @@
+"""BASELINE configs 3 and 4 at their full sizes through the real ring executor
+(W virtual ranks on the one test GPU: PG_TRANSPORT_THREADS keeps the plan,
+executor, streams, events, staging and the gfx950 kernel of the RCCL path and
+replaces only the hop by a device copy).
+
+At these sizes the C oracle would need minutes, so the expected blocks are
+computed on the GPU with torch from the same inputs, in the fold order the
+oracle restates (orc_ring_step, part g of block b: x[b+d] op x[b+2d] op ...
+op x[b]): one IEEE operation per element and step, so double results are
+compared bit for bit; int32 wraps in two's complement on both sides.
+
+  config 3: 4 ranks, int32 sum, 1 GiB per rank, 256 MiB blocks
+  config 4: 8 ranks, double sum, 4 GiB per rank, 512 MiB blocks
+"""
+import ctypes
+
+import pytest
+
+import pgamd
+from gpu_util import ptr
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected_block(torch, xs, b, off, ln, rings, world, op, oracle):
+    out = torch.empty(ln, dtype=xs[0].dtype, device="cuda")
+    for g in range(rings):
+        lo, hi = -(-g * ln // rings), -(-(g + 1) * ln // rings)
+        if lo == hi:
+            continue
+        d = oracle.ring_step(world, rings, g) % world
+        acc = xs[(b + d) % world][off + lo:off + hi].clone()
+        for j in range(2, world + 1):
+            src = xs[(b + j * d) % world][off + lo:off + hi]
+            if op == pgamd.OP_SUM:
+                acc.add_(src)
+            else:
+                acc.mul_(src)
+        out[lo:hi] = acc
+    return out
+
+
+@pytest.mark.parametrize("world,dt,count,rings", [
+    (4, pgamd.DT_INT32, 1 << 28, 2),        # config 3
+    (8, pgamd.DT_DOUBLE, 1 << 29, 2),       # config 4
+    (8, pgamd.DT_DOUBLE, 1 << 29, 4),       # config 4 over four rings
+])
+def test_baseline_config_full_size(gpu, lib, oracle, world, dt, count, rings):
+    torch = gpu
+    g = torch.Generator(device="cuda").manual_seed(31 * world + rings)
+    if dt == pgamd.DT_INT32:
+        xs = [torch.randint(-2**31, 2**31 - 1, (count,), dtype=torch.int32, device="cuda", generator=g)
+              for _ in range(world)]
+    else:
+        xs = [torch.rand(count, dtype=torch.float64, device="cuda", generator=g) * 2 - 1 for _ in range(world)]
+    outs = []
+    for r in range(world):
+        _, ln = pgamd.block_range(count, world, r)
+        outs.append(torch.empty(max(ln, 1), dtype=xs[0].dtype, device="cuda"))
+    torch.cuda.synchronize()
+    sp = (ctypes.c_void_p * world)(*[ptr(x) for x in xs])
+    rp = (ctypes.c_void_p * world)(*[ptr(o) for o in outs])
+    rc = lib.pgx_sim_run(world, pgamd.PG_COLL_REDUCE_SCATTER, sp, rp, count, dt, pgamd.OP_SUM, 4 << 20, 4096, 4,
+                         rings)
+    assert rc == 0, pgamd.last_error()
+    for r in range(world):
+        off, ln = pgamd.block_range(count, world, r)
+        want = _expected_block(torch, xs, r, off, ln, rings, world, pgamd.OP_SUM, oracle)
+        got = outs[r][:ln]
+        if dt == pgamd.DT_DOUBLE:                 # bits, not values (-0.0 == 0.0)
+            got, want = got.view(torch.int64), want.view(torch.int64)
+        assert torch.equal(got, want), (world, dt, rings, r)
+        del want
+    del xs, outs
+    torch.cuda.empty_cache()
