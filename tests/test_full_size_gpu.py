@@ -10,7 +10,8 @@ op x[b]): one IEEE operation per element and step, so double results are
 compared bit for bit; int32 wraps in two's complement on both sides.
 
   config 3: 4 ranks, int32 sum, 1 GiB per rank, 256 MiB blocks
-  config 4: 8 ranks, double sum, 4 GiB per rank, 512 MiB blocks
+  config 4: 8 ranks, double sum, 4 GiB per rank, 512 MiB blocks (2 and 4 rings)
+  config 5: 8 ranks, int32 / double product, 4 KiB calls around 2 GiB calls
 """
 import ctypes
 
@@ -73,3 +74,38 @@ def test_baseline_config_full_size(gpu, lib, oracle, world, dt, count, rings):
         del want
     del xs, outs
     torch.cuda.empty_cache()
+
+
+def test_baseline_config5_sequence(gpu, lib, oracle):
+    """config 5: 8 ranks, int32 and double products, eager-size calls (4 KiB)
+    interleaved with 2 GiB calls on one set of handles (pgx_sim_run opens
+    fresh ones per call; the eager one-shot path and the ring both run)."""
+    torch = gpu
+    world = 8
+    g = torch.Generator(device="cuda").manual_seed(55)
+    for dt, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
+        small = 4096 // pgamd.ELEM_SIZE[dt]
+        for count in (small, big, small):
+            if dt == pgamd.DT_INT32:
+                xs = [torch.randint(-2**31, 2**31 - 1, (count,), dtype=torch.int32, device="cuda", generator=g)
+                      for _ in range(world)]
+            else:   # 1 + U[-2^-10, 2^-10): stays normal over 8 factors (SURVEY.md §8d)
+                xs = [1 + (torch.rand(count, dtype=torch.float64, device="cuda", generator=g) * 2 - 1) * 2.0**-10
+                      for _ in range(world)]
+            outs = [torch.empty(max(pgamd.block_range(count, world, r)[1], 1), dtype=xs[0].dtype, device="cuda")
+                    for r in range(world)]
+            torch.cuda.synchronize()
+            sp = (ctypes.c_void_p * world)(*[ptr(x) for x in xs])
+            rp = (ctypes.c_void_p * world)(*[ptr(o) for o in outs])
+            rc = lib.pgx_sim_run(world, pgamd.PG_COLL_REDUCE_SCATTER, sp, rp, count, dt, pgamd.OP_PROD, 4 << 20,
+                                 4096, 4, 2)
+            assert rc == 0, pgamd.last_error()
+            for r in range(world):
+                off, ln = pgamd.block_range(count, world, r)
+                want = _expected_block(torch, xs, r, off, ln, 2, world, pgamd.OP_PROD, oracle)
+                got = outs[r][:ln]
+                if dt == pgamd.DT_DOUBLE:
+                    got, want = got.view(torch.int64), want.view(torch.int64)
+                assert torch.equal(got, want), (dt, count, r)
+            del xs, outs
+            torch.cuda.empty_cache()
