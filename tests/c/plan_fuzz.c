@@ -1,6 +1,6 @@
 /* tests/c/plan_fuzz.c -- the ring planner (csrc/pg_plan.c, pure C) under
  * AddressSanitizer + UndefinedBehaviorSanitizer: every shape in the grid below
- * is planned for every rank, in one and two rings, reduce-scatter (plain and
+ * is planned for every rank, in one to four rings, reduce-scatter (plain and
  * in place) and all-gather, and every offset a step names must lie inside the
  * buffer it names.  Built and run by tests/test_plan_sanitize.py.  Exit 0 = ok. */
 #include <stdio.h>
@@ -17,7 +17,7 @@ int main(void) {
         for (int cbi = 0; cbi < 5; ++cbi)
           for (int eager = 0; eager <= 4096; eager += 4096)
             for (int infl = 1; infl <= 3; ++infl)
-              for (int rings = 1; rings <= 2; ++rings)
+              for (int rings = 1; rings <= 4; ++rings)
                 for (int alias = 0; alias < 2; ++alias)
                   for (int r = 0; r < W; ++r) {
                     int n = pg_plan_reduce_scatter(r, W, counts[ci], dt, cbs[cbi], eager, infl, rings, alias, NULL, 0);
@@ -27,12 +27,13 @@ int main(void) {
                     if (m != n) return 2;
                     /* the plan must name only in-range offsets */
                     size_t es = dt ? 8 : 4, blk = ((size_t)counts[ci] + W - 1) / W;
+                    size_t stage = (size_t)rings * ((blk + rings - 1) / rings);   /* staging block, elements */
                     for (int i = 0; i < n; ++i) {
                       if (st[i].send_buf == PG_BUF_SRC && (size_t)(st[i].send_off + st[i].send_bytes) > counts[ci] * es) return 3;
                       if ((st[i].send_buf == PG_BUF_STAGE0 || st[i].send_buf == PG_BUF_STAGE1) &&
-                          (size_t)(st[i].send_off + st[i].send_bytes) > blk * es) return 4;
+                          (size_t)(st[i].send_off + st[i].send_bytes) > stage * es) return 4;
                       if ((st[i].recv_buf == PG_BUF_STAGE0 || st[i].recv_buf == PG_BUF_STAGE1) &&
-                          (size_t)(st[i].recv_off + st[i].recv_bytes) > blk * es) return 5;
+                          (size_t)(st[i].recv_off + st[i].recv_bytes) > stage * es) return 5;
                       if (st[i].recv_buf == PG_BUF_OUT && (size_t)(st[i].recv_off + st[i].recv_bytes) > blk * es) return 6;
                     }
                     total += n;

@@ -68,7 +68,7 @@ int main(void) {
       {8, 65541, 1, 0, 1 << 14, 4}, {8, 3, 0, 0, 64, 1}, {6, 2, 1, 1, 8, 2}, {4, 512, 1, 0, 4096, 4}};
   for (size_t i = 0; i < sizeof(shapes) / sizeof(shapes[0]); ++i)
     for (int coll = 0; coll < 3; ++coll)
-      for (int rings = 1; rings <= 2; ++rings)
+      for (int rings = 1; rings <= 4; rings += (rings == 2 ? 2 : 1))
         for (int on_dev = 0; on_dev < 2; ++on_dev)
           for (int eager = 0; eager <= 4096; eager += 4096) {
             const int *s = shapes[i];
