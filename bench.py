@@ -521,6 +521,19 @@ def native_crosscheck(lib, h, rank, world, x_full, dt_full):
     return res
 
 
+def _phases(h, rank, world):
+    """pg_get_stats of the last call, slowest rank per field: where the time of
+    one reduce-scatter goes (device part of the ring, or the xgmi transport's
+    sync / copy / barrier / fold phases) and the bytes a rank received."""
+    st = pgamd.stats(h)
+    keys = ("wall_us", "ring_us", "sync_us", "copy_us", "barrier_us", "kernel_us")
+    out = {k: round(max_over_ranks(float(st[k]), world), 1) for k in keys}
+    out["bytes_recv_per_rank"] = int(st["bytes_recv"])
+    t = out["kernel_us"] or out["ring_us"]
+    out["recv_gbs_per_rank"] = round(st["bytes_recv"] / t / 1e3, 1) if t else None
+    return out
+
+
 def _ring_variant(lib, rank, world, x, out, count, dt, rings, port_off):
     """The same timed reduce-scatter with PG_RINGS=`rings` (a second handle and
     RCCL communicator): rings = 1 shows what the counter-rotating second ring
@@ -609,6 +622,7 @@ def ring_leg(lib, args, rank, world, transport, sink):
         progress(rank, f"  {transport}: timed reduce-scatter")
         wall = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, args.ring_steps, world)
         payload = count * es                       # per rank
+        res["last_call_phases"] = _phases(h, rank, world)
         res.update({"ms_per_reduce_scatter": round(wall * 1e3, 3),
                     "algbw_gibs": round(payload / wall / GIB, 2),
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
