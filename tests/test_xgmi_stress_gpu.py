@@ -46,9 +46,10 @@ def _sequence(seed, world):
     return seq
 
 
-def _worker(rank, world, port, q, mode, seed):
+def _worker(rank, world, port, q, mode, seed, rings):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE=mode)
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE=mode,
+                      PG_RINGS=str(rings))
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -75,7 +76,7 @@ def _worker(rank, world, port, q, mode, seed):
             on_dev = mem == "dev" or (mem == "mixed" and rank % 2 == 0)
             xs = [orc.fill(count, dt, op, 9000 + 31 * i + r) for r in range(world)]
             if coll == "rs":
-                want = orc.ring_reduce_scatter(xs, dt, op)[rank]
+                want = orc.ring_reduce_scatter(xs, dt, op, rings)[rank]
                 recv = np.zeros(max(want.size, 1), NP[dt])
             elif coll == "ag":
                 want = orc.ring_all_gather(xs, dt)[rank]
@@ -83,7 +84,7 @@ def _worker(rank, world, port, q, mode, seed):
                 if in_place:
                     recv[rank * count:(rank + 1) * count] = xs[rank]
             else:
-                want = orc.ring_all_reduce(xs, dt, op)[rank]
+                want = orc.ring_all_reduce(xs, dt, op, rings)[rank]
                 recv = xs[rank].copy() if in_place else np.zeros(max(count, 1), NP[dt])
                 if recv.size == 0:
                     recv = np.zeros(1, NP[dt])
@@ -122,13 +123,14 @@ def _worker(rank, world, port, q, mode, seed):
     q.put((rank, fails))
 
 
-@pytest.mark.parametrize("world,mode,seed", [(4, "read", 1), (3, "push", 2), (8, "read", 3), (5, "read", 4)])
-def test_xgmi_random_sequence(gpu, world, mode, seed):
+@pytest.mark.parametrize("world,mode,seed,rings", [(4, "read", 1, 2), (3, "push", 2, 2), (8, "read", 3, 2),
+                                                   (5, "read", 4, 2), (8, "push", 5, 4), (5, "read", 6, 3)])
+def test_xgmi_random_sequence(gpu, world, mode, seed, rings):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, seed)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, seed, rings)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
