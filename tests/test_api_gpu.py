@@ -343,3 +343,36 @@ def test_all_gather_in_place(gpu, lib, oracle, world, count, eager):
             for r in range(world):
                 got = to_host(torch, R[r]) if on_dev else R[r]
                 assert got.tobytes() == want[r].tobytes(), (world, count, eager, dt, on_dev, r)
+
+
+def test_ring_random_sim(gpu, lib, oracle):
+    """150 random shapes through the ring executor and the eager one-shot path
+    (virtual ranks): world, collective, type, op, count, segment size, eager
+    limit, inflight, rings and buffer kind drawn from one seed; every rank's
+    result bit for bit against the oracle's ring simulator."""
+    rng = np.random.default_rng(2024)
+    for i in range(150):
+        world = int(rng.choice([2, 3, 4, 5, 6, 7, 8, 16]))
+        coll = int(rng.integers(3))
+        dt, op = int(rng.integers(2)), int(rng.integers(2))
+        count = int(rng.choice([0, 1, 2, world - 1, world + 1, 97, 1000, 4099, 65537, 300007]))
+        cb = int(rng.choice([4, 12, 64, 1000, 4096, 1 << 16, 4 << 20]))
+        eager = int(rng.choice([0, 4096]))
+        infl = int(rng.integers(1, 9))
+        rings = int(rng.integers(1, 5))
+        on_dev = bool(rng.integers(2))
+        xs = [oracle.fill(count, dt, op, 50000 + 97 * i + r) for r in range(world)]
+        if coll == pgamd.PG_COLL_REDUCE_SCATTER:
+            want = oracle.ring_reduce_scatter(xs, dt, op, rings)
+            recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want]
+        elif coll == pgamd.PG_COLL_ALL_GATHER:
+            want = oracle.ring_all_gather(xs, dt)
+            recvs = [np.zeros(max(count * world, 1), NP[dt]) for _ in range(world)]
+        else:
+            want = oracle.ring_all_reduce(xs, dt, op, rings)
+            recvs = [np.zeros(max(count, 1), NP[dt]) for _ in range(world)]
+        sends = [x if x.size else np.zeros(1, NP[dt]) for x in xs]
+        got = sim(lib, gpu, coll, sends, recvs, count, dt, op, cb, eager, infl, on_dev, rings)
+        case = (i, world, coll, dt, op, count, cb, eager, infl, rings, on_dev)
+        for r in range(world):
+            assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (case, r)
