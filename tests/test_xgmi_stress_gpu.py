@@ -20,7 +20,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 COUNTS = (0, 1, 5, 64, 1000, 4099, 65539, 300001, (1 << 20) + 7)
-CALLS = 120
+CALLS = int(os.environ.get("XGMI_STRESS_CALLS", "120"))    # a soak run sets more
 
 
 def _free_port():
