@@ -62,6 +62,10 @@ struct xgmi_ctx {
   void *bar;                    /* node-local shm barrier (pg_boot.c), or NULL */
   int zc;                       /* zero-copy inputs allowed (PG_XGMI_ZERO_COPY) */
   int push;                     /* PG_XGMI_MODE=push: reduce-scatter writes, not reads */
+  int force_copy;               /* this call: no zero-copy (the retry after a failed import) */
+  long fail_import_at;          /* test hook PG_XGMI_FAIL_IMPORT=n: the n-th import fails */
+  long imports;                 /* imports attempted so far (for the hook)   */
+  long retries;                 /* calls redone with the slot copy            */
   hipIpcMemHandle_t exp_h;      /* last export of a caller allocation       */
   unsigned long long exp_bid;
   void *exp_base;
@@ -233,6 +237,8 @@ int pg_xport_xgmi_init(struct pg *pg) {
     return -1;
   }
   x->push = e && strcmp(e, "push") == 0;
+  e = getenv("PG_XGMI_FAIL_IMPORT");
+  x->fail_import_at = (e && *e) ? atol(e) : 0;
   x->imp = (struct xg_import *)calloc((size_t)pg->world_size * XG_IMPORTS, sizeof(struct xg_import));
   if (!x->imp) { pg_set_error("xgmi: out of host memory"); return -1; }
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
@@ -394,7 +400,8 @@ static const char *import_input(struct xgmi_ctx *x, int q, const struct xg_desc 
     if (e[i].stamp < e[lru].stamp) lru = i;
   if (e[lru].base) { hipIpcCloseMemHandle(e[lru].base); e[lru].base = NULL; }
   void *p = NULL;
-  hipError_t err = hipIpcOpenMemHandle(&p, d->h, hipIpcMemLazyEnablePeerAccess);
+  hipError_t err = ++x->imports == x->fail_import_at ? hipErrorInvalidValue
+                                                     : hipIpcOpenMemHandle(&p, d->h, hipIpcMemLazyEnablePeerAccess);
   if (err != hipSuccess) {
     (void)hipGetLastError();
     pg_set_error("xgmi: hipIpcOpenMemHandle(rank %d's input, bid %llu): %s", q, (unsigned long long)d->bid,
@@ -431,7 +438,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   im->stats.sync_us += t1 - t0;
   if (x->zc && x->bar && bytes) {
     struct xg_desc mine;
-    if (!in_dev || may_alias_out || !export_input(x, in, &mine)) memset(&mine, 0, sizeof(mine));
+    if (!in_dev || may_alias_out || x->force_copy || !export_input(x, in, &mine)) memset(&mine, 0, sizeof(mine));
     mine.nbytes = bytes;
     pg_trace(pg, "xgmi share: input %p exported=%d (bid %llu base %#llx size %llu)", in, mine.ok,
              (unsigned long long)mine.bid, (unsigned long long)mine.base, (unsigned long long)mine.size);
@@ -466,7 +473,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
         pg_trace(pg, "xgmi share: rank %d's input at %p (bid %llu base %#llx size %llu off %llu)", q,
                  (const void *)by_rank[q], (unsigned long long)all[q].bid, (unsigned long long)all[q].base,
                  (unsigned long long)all[q].size, (unsigned long long)all[q].off);
-        if (!by_rank[q]) *fail = 1;           /* error set by import_input */
+        if (!by_rank[q]) *fail = 2;           /* soft: every rank redoes the call with the slot copy */
       }
       *zero_copy = 1;
       return 0;
@@ -502,15 +509,17 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
 }
 
 /* End of a call: zero-copy inputs stay untouched until every peer is done.
- * That closing barrier also carries each rank's result, so a rank that could
- * not map a peer, allocate, or launch its fold fails the call on every rank:
- * callers see the same return code everywhere and stay in step.  Slot-copy
- * calls meet here too (one more node-local barrier, ~1 us) for the same
- * guarantee; only the TCP-barrier fallback (PG_NO_SHM_BARRIER=1, never
- * zero-copy) leaves a local failure local. */
+ * That closing barrier also carries each rank's status (0 ok, 1 failed, 2
+ * could not map a peer's input), so a failure on one rank is seen by every
+ * rank and the callers stay in step.  Returns 0, -1 (some rank failed), or 1
+ * (some rank could not map a peer, none failed otherwise: the caller redoes
+ * the call on every rank with the slot copy, see xgmi_retry).  Slot-copy
+ * calls meet here too (one more node-local barrier, ~1 us); only the
+ * TCP-barrier fallback (PG_NO_SHM_BARRIER=1, never zero-copy) leaves a local
+ * failure local. */
 static int finish(struct pg *pg, int zero_copy, int fail) {
   struct xgmi_ctx *x = ctx_of(pg);
-  int rc = 0, any = fail;
+  int rc = 0, hard = fail == 1, soft = fail == 2;
   if (x->bar) {
     struct pg_impl *im = (struct pg_impl *)pg->impl;
     volatile int32_t *flags = (volatile int32_t *)((char *)x->bar + XG_FLAG_OFF) + (x->gen & 1) * 16;
@@ -518,13 +527,17 @@ static int finish(struct pg *pg, int zero_copy, int fail) {
     double t = us_now();
     rc = barrier(pg);
     im->stats.barrier_us += us_now() - t;
-    for (int q = 0; q < pg->world_size && !rc; ++q) any |= flags[q];
-    if (any && !fail && !rc) pg_set_error("xgmi: a peer failed this call");
+    for (int q = 0; q < pg->world_size && !rc; ++q) {
+      hard |= flags[q] == 1;
+      soft |= flags[q] == 2;
+    }
+    if (hard && fail != 1 && !rc) pg_set_error("xgmi: a peer failed this call");
   } else if (zero_copy) {
     rc = barrier(pg);
   }
   x->gen++;
-  return (rc || any) ? -1 : 0;
+  if (rc || hard) return -1;
+  return soft ? 1 : 0;
 }
 
 /* out = fold over ranks of this rank's block (at off_elems, len elements),
@@ -645,7 +658,7 @@ static int push_inputs(struct pg *pg, const char *in, int count, int dt, int can
   return 0;
 }
 
-int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+static int rs_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
@@ -667,7 +680,8 @@ int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int coun
     out = im->dout;
   }
   if (!fail && fold_block(pg, out, by_rank, fold_off, len, dt, op)) fail = 1;
-  if (finish(pg, zc, fail)) return -1;
+  int fin = finish(pg, zc, fail);
+  if (fin) return fin;
   if (!rd && len && pg_copy_parallel(recvbuf, out, len * es)) return -1;
   return 0;
 }
@@ -699,7 +713,7 @@ static int gather(struct pg *pg, char *full, const char *const *by_rank, int cou
   return 0;
 }
 
-int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+static int ag_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t es = pg_elem_size(dt), slot_bytes = (size_t)count * es, total = slot_bytes * (size_t)pg->world_size;
   int rd = is_dev(recvbuf), zc, fail;
@@ -714,13 +728,14 @@ int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     full = (char *)im->dout;
   }
   if (!fail && gather(pg, full, by_rank, count, 1, dt)) fail = 1;
-  if (finish(pg, zc, fail)) return -1;
+  int fin = finish(pg, zc, fail);
+  if (fin) return fin;
   if (!rd && total && pg_copy_parallel(recvbuf, full, total)) return -1;
   im->stats.bytes_recv += (int64_t)(total - slot_bytes);
   return 0;
 }
 
-int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+static int ar_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, off, len;
@@ -768,9 +783,46 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
     for (int q = 0; q < pg->world_size; ++q) res_by_rank[q] = slot(x, XG_REG_R, q, which);
     if (!fail && gather(pg, full, res_by_rank, count, 0, dt)) fail = 1;
   }
-  if (finish(pg, zc, fail)) return -1;
+  int fin = finish(pg, zc, fail);
+  if (fin) return fin;
   if (!rd && bytes && pg_copy_parallel(recvbuf, full, bytes)) return -1;
   return 0;
+}
+
+/* A call some rank could not zero-copy (a peer's input failed to map: an IPC
+ * open that ROCm refused) is redone once on every rank with the slot copy,
+ * which needs no mapping of caller memory; every rank learned of it at the
+ * same closing barrier, so all of them retry.  The first attempt wrote
+ * nothing that the retry does not overwrite (in-place calls never take
+ * zero-copy). */
+static int xgmi_retry(struct pg *pg, int first) {
+  struct xgmi_ctx *x = ctx_of(pg);
+  if (first != 1) return first;
+  x->force_copy = 1;
+  x->retries++;
+  pg_trace(pg, "xgmi: a peer's input could not be mapped; redoing the call with the slot copy");
+  return 0;
+}
+
+int pg_xgmi_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  int rc = rs_once(pg, sendbuf, recvbuf, count, dt, op);
+  if (rc == 1 && xgmi_retry(pg, rc) == 0) rc = rs_once(pg, sendbuf, recvbuf, count, dt, op);
+  ctx_of(pg)->force_copy = 0;
+  return rc == 0 ? 0 : -1;
+}
+
+int pg_xgmi_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+  int rc = ag_once(pg, sendbuf, recvbuf, count, dt);
+  if (rc == 1 && xgmi_retry(pg, rc) == 0) rc = ag_once(pg, sendbuf, recvbuf, count, dt);
+  ctx_of(pg)->force_copy = 0;
+  return rc == 0 ? 0 : -1;
+}
+
+int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  int rc = ar_once(pg, sendbuf, recvbuf, count, dt, op);
+  if (rc == 1 && xgmi_retry(pg, rc) == 0) rc = ar_once(pg, sendbuf, recvbuf, count, dt, op);
+  ctx_of(pg)->force_copy = 0;
+  return rc == 0 ? 0 : -1;
 }
 
 /* ---- link probe ----------------------------------------------------------------
