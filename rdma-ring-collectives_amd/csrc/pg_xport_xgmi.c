@@ -35,6 +35,7 @@
 #define XG_REG_X 0              /* contribution slots X0, X1 */
 #define XG_REG_R 1              /* all-reduce result slots R0, R1 */
 #define XG_IMPORTS 2            /* mapped input allocations cached per peer */
+#define XG_FOLD_ONE_LAUNCH_MAX (256u << 10)   /* blocks up to this size fold all ring parts in one launch */
 
 struct xg_import {
   unsigned long long bid;
@@ -551,7 +552,19 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
   size_t es = pg_elem_size(dt);
   double tk = us_now();
   pg_trace(pg, "xgmi fold: %zu elements from %d ranks", len, W);
-  for (int g = 0; g < im->rings; ++g) {
+  const int one_launch = im->rings > 1 && len * es <= XG_FOLD_ONE_LAUNCH_MAX;
+  if (one_launch) {
+    /* small block: every ring part in one launch.  pgk_fold_blocks folds block
+     * 0 of its sources as src[d] op src[2d] op ... op src[0] per part; with
+     * src[j] = rank (r+j)'s block that is exactly the loop below. */
+    const void *srcs[16];
+    for (int j = 0; j < W; ++j) srcs[j] = by_rank[(r + j) % W] + off_elems * es;
+    if (pgk_fold_blocks(out, srcs, W, len, len, im->rings, dt, op, (void *)im->red)) {
+      pg_set_error("xgmi: %s", pgk_last_error());
+      return -1;
+    }
+  }
+  for (int g = 0; g < im->rings && !one_launch; ++g) {
     size_t po, pl;
     pg_block_part(len, im->rings, g, &po, &pl);
     if (!pl) continue;
