@@ -124,11 +124,13 @@ PG_API int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *
                 size_t eager_max, int inflight, int rings);
 
 /* The hot path with both operands in host memory: dst[i] = dst[i] op src[i]
- * (op: OP_SUM / OP_PROD), staged through HBM in chunk_bytes pieces (0 =
- * 16 MiB) that flow through 3 device slots: uploads (dst, src) and the reduce
- * run on the calling thread while a helper thread downloads finished pieces,
- * so both PCIe directions are busy at once.  Synchronous.  This is what the
- * PCIe-inclusive rate in DESIGN.md measures. */
+ * (op: OP_SUM / OP_PROD).  Both operands pinned and mapped (hipHostMalloc,
+ * hipHostRegister): one reduce kernel works on them in place across PCIe,
+ * reading and writing at once.  Otherwise staged through HBM in chunk_bytes
+ * pieces (0 = 16 MiB) that flow through 3 device slots: uploads (dst, src)
+ * and the reduce run on the calling thread while a helper thread downloads
+ * finished pieces.  Synchronous.  This is what the PCIe-inclusive rate in
+ * DESIGN.md measures. */
 PG_API int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
 
 /* Measurements of the last collective on this handle. */

@@ -1,7 +1,9 @@
 /*
  * pg_host.c -- the chunk reduce with both operands in host memory
  * (pgx_reduce_host, include/pg_ext.h): the PCIe-inclusive form of the hot path
- * that DESIGN.md §8 reports beside the device-resident rate.
+ * that DESIGN.md §8 reports beside the device-resident rate.  Pinned, mapped
+ * operands are reduced in place by one kernel over PCIe; pageable ones flow
+ * through HBM slots.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -71,11 +73,48 @@ static void *hp_downloader(void *arg) {
   return NULL;
 }
 
+/* The device address of [p, p+bytes) when it lies inside one pinned, mapped
+ * host allocation (hipHostMalloc, hipHostRegister), else NULL.  Only such
+ * memory may be touched by a kernel: pageable memory would fault (no XNACK). */
+static void *mapped_host(const void *p, size_t bytes) {
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof(a));
+  void *d = NULL, *start = NULL;
+  size_t size = 0;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost ||
+      hipHostGetDevicePointer(&d, (void *)p, 0) != hipSuccess || !d ||
+      hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return NULL;
+  }
+  const char *lo = (const char *)start, *q = (const char *)p;
+  if (!lo || q < lo || bytes > size || (size_t)(q - lo) > size - bytes) return NULL;
+  return d;
+}
+
+/* Both operands pinned and mapped: one reduce launch on their device
+ * addresses.  The kernel reads dst and src across PCIe and writes dst back
+ * itself, so both link directions carry data at once; the staged pipeline's
+ * SDMA copies run one direction at a time (tools/lab/host_direct_probe.py,
+ * 256 MiB double sum: 10.1 ms direct vs 13.4 ms staged). */
+static int reduce_host_direct(void *ddst, const void *dsrc, size_t n, int datatype, int op) {
+  if (pgk_reduce(ddst, dsrc, n, datatype, op, NULL)) {
+    pg_set_error("pgx_reduce_host: %s", pgk_last_error());
+    return -1;
+  }
+  hipError_t e = hipStreamSynchronize(NULL);
+  if (e != hipSuccess) { pg_set_error("pgx_reduce_host: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
 int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes) {
   size_t es = pg_elem_size(datatype);
   if (!es || (op != PGK_OP_SUM && op != PGK_OP_PROD)) { pg_set_error("pgx_reduce_host: bad datatype/op"); return -1; }
   if (!n) return 0;
   if (!dst || !src) { pg_set_error("pgx_reduce_host: NULL buffer"); return -1; }
+  void *ddst = mapped_host(dst, n * es), *dsrc = mapped_host(src, n * es);
+  if (ddst && dsrc) return reduce_host_direct(ddst, dsrc, n, datatype, op);
   size_t piece = chunk_bytes >= (1u << 20) ? chunk_bytes : HP_PIECE_DEFAULT;
   struct hp_ctx c;
   memset(&c, 0, sizeof(c));

@@ -199,6 +199,39 @@ def test_reduce_host_staged(gpu, lib, oracle):
     assert lib.pgx_reduce_host(None, None, 5, 3, 0, 0) == -1
 
 
+def test_reduce_host_pinned_direct(gpu, lib, oracle):
+    """pgx_reduce_host with both operands pinned and mapped (hipHostMalloc):
+    one kernel reduces them in place over PCIe.  Offsets inside the pinned
+    allocations, odd lengths, and a pinned dst with a pageable src (which must
+    take the staged path: a kernel may not touch pageable memory)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    cap = (3 << 20) * 8 + 4096
+    ptrs = []
+    for _ in range(2):
+        p = ctypes.c_void_p()
+        assert hip.hipHostMalloc(ctypes.byref(p), cap, 0x2) == 0      # hipHostMallocMapped
+        ptrs.append(p.value)
+    try:
+        for dt, op, n, off in ((1, 0, 3 << 20, 0), (0, 1, (3 << 20) + 1, 4), (1, 1, 1001, 8), (0, 0, 7, 12)):
+            es = 8 if dt else 4
+            a, b = oracle.fill(n, dt, op, 61), oracle.fill(n, dt, op, 62)
+            want = oracle.reduce(a, b, dt, op)
+            ctypes.memmove(ptrs[0] + off, a.ctypes.data, n * es)
+            ctypes.memmove(ptrs[1] + off, b.ctypes.data, n * es)
+            assert lib.pgx_reduce_host(ptrs[0] + off, ptrs[1] + off, n, dt, op, 0) == 0, pgamd.last_error()
+            assert ctypes.string_at(ptrs[0] + off, n * es) == want.tobytes(), (dt, op, n, off)
+            assert ctypes.string_at(ptrs[1] + off, n * es) == b.tobytes()
+            ctypes.memmove(ptrs[0] + off, a.ctypes.data, n * es)            # pinned dst, pageable src
+            assert lib.pgx_reduce_host(ptrs[0] + off, b.ctypes.data, n, dt, op, 0) == 0, pgamd.last_error()
+            assert ctypes.string_at(ptrs[0] + off, n * es) == want.tobytes()
+    finally:
+        for p in ptrs:
+            hip.hipHostFree(p)
+
+
 @pytest.mark.parametrize("dt,op", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_reduce_multi_fold_order(gpu, lib, oracle, dt, op):
     """pgk_reduce_multi folds left to right: equal to nsrc-1 successive
