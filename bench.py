@@ -343,9 +343,10 @@ def host_leg(lib, reps=3):
                      "payload_gibs": round(n * 8 / dt_ / GIB, 2),
                      "pcie_gbs": round(3 * n * 8 / dt_ / 1e9, 2)}
         del d, s_
-    out["note"] = ("256 MiB double sum, dst/src in host memory: 16 MiB pieces through 3 HBM slots, H2D dst+src "
-                   "and the reduce on one thread, D2H dst on another (both PCIe directions at once); pcie_gbs "
-                   "counts the 3*n*8 bytes that cross PCIe")
+    out["note"] = ("256 MiB double sum, dst/src in host memory (pgx_reduce_host). pageable: 16 MiB pieces through "
+                   "3 HBM slots, H2D dst+src and the reduce on one thread, D2H dst on another; pinned: one reduce "
+                   "kernel on the mapped host pointers, reading and writing across PCIe at once. pcie_gbs counts "
+                   "the 3*n*8 bytes that cross PCIe")
     return out
 
 
