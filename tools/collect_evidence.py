@@ -37,6 +37,10 @@ def main():
         if (OUT / f"bench_n{w}.log").exists():
             (PROF / f"{tag}_bench_n{w}_onegpu_rehearsal.json").write_text(
                 json.dumps(first_json(OUT / f"bench_n{w}.log")) + "\n")
+    for src, dst in (("host_direct.log", f"{tag}_host_direct_probe.txt"), ("gather.log", f"{tag}_gather_probe.txt")):
+        if (OUT / src).exists():
+            (PROF / dst).write_text("".join(l + "\n" for l in (OUT / src).read_text().splitlines()
+                                            if "amdgpu.ids" not in l))
     if (OUT / "host_pipe.log").exists():
         (PROF / f"{tag}_host_pipe_probe.txt").write_text(
             "".join(l + "\n" for l in (OUT / "host_pipe.log").read_text().splitlines() if "amdgpu.ids" not in l))

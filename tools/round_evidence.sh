@@ -18,3 +18,5 @@ PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n4 500 python -m torch.distributed.ru
 PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
   --master-addr 127.0.0.1 --master-port 29553 bench.py --gpus 8 --steps 10 --warmup 2 --transports xgmi,xgmi_push --ring-timeout 500
 tools/gpu_step.sh host_pipe 300 python tools/host_pipe_probe.py
+tools/gpu_step.sh host_direct 120 python tools/lab/host_direct_probe.py 256
+tools/gpu_step.sh gather 200 python tools/lab/gather_probe.py 8 64 256
