@@ -22,6 +22,12 @@
  * buffering makes one barrier per call enough: a slot is rewritten two calls
  * later, and every rank passed the intervening call's barrier only after
  * finishing its reads.
+ *
+ * Every call closes at a barrier that carries each rank's status (finish), so
+ * outcomes are collective: a failure anywhere fails the call everywhere, and a
+ * peer input that could not be mapped makes every rank redo the call with the
+ * slot copy (xgmi_retry).  Descriptors carry the byte count, so ranks called
+ * with different counts fail before reading anything.
  */
 #include <stdint.h>
 #include <stdio.h>
