@@ -109,3 +109,28 @@ def test_baseline_config5_sequence(gpu, lib, oracle):
                 assert torch.equal(got, want), (dt, count, r)
             del xs, outs
             torch.cuda.empty_cache()
+
+
+def test_maximum_count_ring(gpu, lib, oracle):
+    """The API's largest count (INT_MAX int32 elements, 8 GiB per rank) through
+    the 2-rank ring: every byte offset of the plan and executor past 2^31 and
+    2^32, the ragged second block (one element shorter), both rings."""
+    torch = gpu
+    world, count = 2, (1 << 31) - 1
+    g = torch.Generator(device="cuda").manual_seed(77)
+    xs = [torch.randint(-2**31, 2**31 - 1, (count,), dtype=torch.int32, device="cuda", generator=g)
+          for _ in range(world)]
+    outs = [torch.empty(pgamd.block_range(count, world, r)[1], dtype=torch.int32, device="cuda")
+            for r in range(world)]
+    torch.cuda.synchronize()
+    sp = (ctypes.c_void_p * world)(*[ptr(x) for x in xs])
+    rp = (ctypes.c_void_p * world)(*[ptr(o) for o in outs])
+    rc = lib.pgx_sim_run(world, pgamd.PG_COLL_REDUCE_SCATTER, sp, rp, count, pgamd.DT_INT32, pgamd.OP_SUM,
+                         64 << 20, 4096, 4, 2)
+    assert rc == 0, pgamd.last_error()
+    for r in range(world):
+        off, ln = pgamd.block_range(count, world, r)
+        want = _expected_block(torch, xs, r, off, ln, 2, world, pgamd.OP_SUM, oracle)
+        assert torch.equal(outs[r], want), r
+    del xs, outs
+    torch.cuda.empty_cache()
