@@ -41,7 +41,9 @@
 #define XG_REG_X 0              /* contribution slots X0, X1 */
 #define XG_REG_R 1              /* all-reduce result slots R0, R1 */
 #define XG_IMPORTS 2            /* mapped input allocations cached per peer */
-#define XG_FOLD_ONE_LAUNCH_MAX (256u << 10)   /* blocks up to this size fold all ring parts in one launch */
+#define XG_FOLD_ONE_LAUNCH_MAX (1u << 20)   /* blocks up to this size fold all ring parts in one launch
+                                               (profiles/r01_fold_launch_probe.txt: one launch wins to 1 MiB,
+                                               ties at 4 MiB, loses at 16 MiB) */
 
 struct xg_import {
   unsigned long long bid;
