@@ -9,7 +9,8 @@
  * which every rank sends each peer what that peer needs, and ONE launch:
  *
  *   reduce-scatter  rank r receives block r of every peer's input and folds
- *                   them with pgk_reduce_multi in ring order;
+ *                   them in ring order, every ring part in one launch
+ *                   (pgk_fold_blocks; pgk_reduce_multi for one ring);
  *   all-gather      every rank sends its slot to every peer;
  *   all-reduce      every rank sends its whole input to every peer and
  *                   pgk_fold_blocks folds each block in its ring order.
@@ -81,23 +82,33 @@ int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int cou
     im->stats.bytes_recv += (int64_t)slot;
   }
   if (im->ops->group_end(im, im->comm)) return -1;
-  for (int g = 0; blen && g < im->rings; ++g) {     /* one launch per ring part of block r */
-    size_t po, pl;
-    pg_block_part(blen, im->rings, g, &po, &pl);
-    if (!pl) continue;
+  if (blen && im->rings > 1) {
+    /* every ring part of block r in one launch: pgk_fold_blocks folds block 0
+     * of its sources part by part in ring order, and source j is rank r+j's
+     * block r (tools/lab/fold_launch_probe.py: 3.8 vs 6.6 us at these sizes) */
     const void *srcs[EAGER_MAX_WORLD];
-    const int d = pg_ring_offset(W, im->rings, g);
     for (int j = 0; j < W; ++j) {
-      int q = ((r + (j + 1) * d) % W + W) % W;                        /* the part's ring order */
-      const char *base = q == r ? src + boff * es : gat + (size_t)q * slot;
-      srcs[j] = base + po * es;
+      int q = (r + j) % W;
+      srcs[j] = q == r ? src + boff * es : gat + (size_t)q * slot;
     }
-    if (pgk_reduce_multi(out + po * es, srcs, W, pl, dt, op, (void *)im->comm)) {
+    if (pgk_fold_blocks(out, srcs, W, blen, blen, im->rings, dt, op, (void *)im->comm)) {
       pg_set_error("%s", pgk_last_error());
       return -1;
     }
     im->stats.reduce_launches++;
-    im->stats.reduce_elems += (int64_t)(pl * (size_t)(W - 1));
+    im->stats.reduce_elems += (int64_t)(blen * (size_t)(W - 1));
+  } else if (blen) {                                 /* one ring: the vector kernel */
+    const void *srcs[EAGER_MAX_WORLD];
+    for (int j = 0; j < W; ++j) {
+      int q = (r + 1 + j) % W;                                          /* the ring order */
+      srcs[j] = q == r ? src + boff * es : gat + (size_t)q * slot;
+    }
+    if (pgk_reduce_multi(out, srcs, W, blen, dt, op, (void *)im->comm)) {
+      pg_set_error("%s", pgk_last_error());
+      return -1;
+    }
+    im->stats.reduce_launches++;
+    im->stats.reduce_elems += (int64_t)(blen * (size_t)(W - 1));
   }
   if (finish(im)) return -1;
   if (out != (char *)recvbuf && pg_timed_copy(recvbuf, out, slot, &im->stats.d2h_us)) return -1;
