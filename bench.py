@@ -530,6 +530,7 @@ def _phases(h, rank, world):
     keys = ("wall_us", "ring_us", "sync_us", "copy_us", "barrier_us", "kernel_us")
     out = {k: round(max_over_ranks(float(st[k]), world), 1) for k in keys}
     out["bytes_recv_per_rank"] = int(st["bytes_recv"])
+    out["zero_copy"] = bool(st["zero_copy"])
     t = out["kernel_us"] or out["ring_us"]
     out["recv_gbs_per_rank"] = round(st["bytes_recv"] / t / 1e3, 1) if t else None
     return out

@@ -146,6 +146,8 @@ struct pg_stats {
   double copy_us;        /* input -> exchange slot (H2D or D2D), synced     */
   double barrier_us;     /* meeting the other ranks                         */
   double kernel_us;      /* fold / gather launch + completion               */
+  int32_t zero_copy;     /* xgmi: 1 = peers read this call's inputs in place */
+  int32_t retried;       /* xgmi: 1 = redone with the slot copy (a peer input failed to map) */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

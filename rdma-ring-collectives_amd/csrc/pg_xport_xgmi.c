@@ -485,6 +485,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
         if (!by_rank[q]) *fail = 2;           /* soft: every rank redoes the call with the slot copy */
       }
       *zero_copy = 1;
+      im->stats.zero_copy = !*fail;
       return 0;
     }
     /* somebody's input cannot be shared in place: everybody copies */
@@ -821,6 +822,7 @@ static int xgmi_retry(struct pg *pg, int first) {
   if (first != 1) return first;
   x->force_copy = 1;
   x->retries++;
+  ((struct pg_impl *)pg->impl)->stats.retried = 1;
   pg_trace(pg, "xgmi: a peer's input could not be mapped; redoing the call with the slot copy");
   return 0;
 }

@@ -351,12 +351,14 @@ def _realloc_worker(rank, world, port, q):
             y = torch.empty(ln, dtype=torch.float64, device="cuda")
             if lib.pg_reduce_scatter(p.value, y.data_ptr(), count, 1, 0, h) != 0:
                 out["fails"].append((trial, pgamd.last_error()))
+            out.setdefault("zero_copy", []).append(pgamd.stats(h)["zero_copy"])
             i = np.arange(off, off + ln)
             want = world * (i % 97) + world * 1000 * trial + world * (world - 1) // 2
             if not np.array_equal(y.cpu().numpy(), want.astype(np.float64)):
                 out["fails"].append((trial, "stale or wrong data"))
             hip.hipFree(p)
         out["same_va"] = len(set(vas)) < len(vas)
+        out["vas"] = vas
         lib.pg_close(h)
     except Exception as e:
         out["fails"].append(("exception", repr(e)))
@@ -384,6 +386,13 @@ def test_xgmi_input_reallocated_at_same_address(gpu):
     for rank, out in results:
         assert not out["fails"], (rank, out)
     assert any(out["same_va"] for _, out in results), "no address was reused: the test did not set up the hazard"
+    # trial t is shared in place unless some rank's allocation recycles an address it exported before
+    # (then every rank takes the slot copy: the choice is collective)
+    trials = len(results[0][1]["vas"])
+    for t in range(trials):
+        recycled = any(out["vas"][t] in out["vas"][:t] for _, out in results)
+        for rank, out in results:
+            assert out["zero_copy"][t] == (0 if recycled else 1), (t, rank, out)
 
 
 def _mismatch_worker(rank, world, port, q, mode):
@@ -482,6 +491,7 @@ def _retry_worker(rank, world, port, q):
                 y = torch.zeros(count * world, dtype=torch.float64, device="cuda")
                 rc = lib.pg_all_gather(x.data_ptr(), y.data_ptr(), count, 1, h)
             out["errs"].append(pgamd.last_error())
+            out.setdefault("retried", []).append(pgamd.stats(h)["retried"])
             if rc != 0 or y.cpu().numpy().tobytes() != want.tobytes():
                 out["fails"].append((i, coll, rc, pgamd.last_error()))
         lib.pg_close(h)
@@ -512,3 +522,5 @@ def test_xgmi_failed_import_is_redone_with_copy(gpu):
         assert not out["fails"], (rank, out)
     errs = dict(results)[1]["errs"]
     assert "hipIpcOpenMemHandle" in errs[0], errs       # the injected failure happened, and was absorbed
+    for rank, out in results:                           # by every rank redoing the first call, only that one
+        assert out["retried"] == [1, 0, 0, 0], (rank, out["retried"])

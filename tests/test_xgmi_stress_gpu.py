@@ -69,6 +69,7 @@ def _worker(rank, world, port, q, mode, seed, rings):
         NP = {0: np.int32, 1: np.float64}
         TD = {0: torch.int32, 1: torch.float64}
         pool = None                                  # a kept device input allocation
+        zc = 0                                       # calls whose inputs peers read in place
         for i, coll, dt, op, count, mem, in_place, keep, flush in _sequence(seed, world):
             if flush:
                 pool = None
@@ -114,10 +115,13 @@ def _worker(rank, world, port, q, mode, seed, rings):
             if rc != 0:
                 fails.append((i, coll, count, mem, "rc", pgamd.last_error()))
                 break
+            zc += pgamd.stats(h)["zero_copy"]
             got = R.cpu().numpy() if on_dev else R
             if got[:want.size].tobytes() != want.tobytes():
                 fails.append((i, coll, dt, op, count, mem, in_place, keep, flush))
         lib.pg_close(h)
+        if mode == "read" and zc == 0:
+            fails.append("no call read its inputs in place: zero-copy never exercised")
     except Exception as e:  # report, never hang the parent
         fails.append(("exception", repr(e)))
     q.put((rank, fails))
