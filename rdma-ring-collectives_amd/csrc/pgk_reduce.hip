@@ -261,10 +261,13 @@ int g_unroll = 0;
 // Measured on MI355X (profiles/r01_sweep_kernel_shapes.csv, kernel-stamped,
 // f64 sum, nt): 512x2 leads below 128 MiB per operand (64 MiB: 31.1 us vs
 // 31.8 us for 1024x1), 1024x1 from 256 MiB up (256 MiB: 121.7 us vs 124.5 us
-// for 512x2; 1 GiB: 495 us vs 515 us).
+// for 512x2; 1 GiB: 495 us vs 515 us).  From 128 MiB to below 256 MiB 256x4
+// leads 1024x1 by 1.3% on two boxes (128 MiB: 63.2 vs 64.1 us,
+// profiles/r01_lab2.txt, profiles/r01_lab4_policy.txt).
 void shape_for(size_t bytes_per_operand, int* block, int* unroll) {
   if (g_block) { *block = g_block; *unroll = g_unroll; return; }
   if (bytes_per_operand < (128u << 20)) { *block = 512; *unroll = 2; }
+  else if (bytes_per_operand < (256u << 20)) { *block = 256; *unroll = 4; }
   else { *block = 1024; *unroll = 1; }
 }
 
