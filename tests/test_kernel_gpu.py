@@ -141,6 +141,28 @@ def test_full_size_config2(gpu, lib, oracle):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("nbytes", [(128 << 20) - 16, 128 << 20, (160 << 20) + 24, (256 << 20) - 8, 256 << 20])
+def test_default_shape_boundaries(gpu, lib, oracle, nbytes):
+    """Each size-chosen vector shape (shape_for in pgk_reduce.hip: 512x2 below
+    128 MiB per operand, 256x4 up to 256 MiB, 1024x1 above) at and around its
+    boundaries, with a ragged tail and a partial last tile, against the oracle;
+    the double sums start one element past the 16-B phase (head element)."""
+    torch = gpu
+    for dt, op in ((1, 0), (0, 1)):
+        es = 4 if dt == 0 else 8
+        n = nbytes // es
+        a, b = oracle.fill(n + 1, dt, op, 41), oracle.fill(n + 1, dt, op, 42)
+        off = 1 if dt == 1 else 0
+        d, s = to_dev(torch, a), to_dev(torch, b)
+        assert lib.pgk_reduce(ptr(d) + off * es, ptr(s) + off * es, n, dt, op, stream(torch)) == 0
+        got = to_host(torch, d)
+        want = a.copy()
+        want[off:off + n] = oracle.reduce(a[off:off + n], b[off:off + n], dt, op)
+        assert got.tobytes() == want.tobytes(), (dt, op, nbytes)
+        del d, s, got
+        torch.cuda.empty_cache()
+
+
 def test_maximum_counts(gpu, lib):
     """The API's largest count (INT_MAX elements, include/pg.h `int count`) on the
     vector path and on the element-wise path (dst one element off src's 16-B
