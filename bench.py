@@ -419,15 +419,16 @@ def _timed_rs(lib, h, x, out, count, dt, op, reps, world):
     return max_over_ranks(time.perf_counter() - t0, world) / reps
 
 
-def _pattern(count, rank, world, dt, op, off=0, ln=None):
+def _pattern(count, rank, world, dt, op, off=0, ln=None, device="cuda"):
     """Inputs whose W-rank reduction is exact in both dtypes, so every rank can
     check its block on the device: sum -> (i % 1000) + rank; prod -> powers of
     two (double) / {1, 2, -1} (int32).  Elements [off, off + ln) of rank
     `rank`'s input (default: all `count`), built in the target dtype without
-    full-size int64 temporaries."""
+    full-size int64 temporaries.  (device="cpu": tests/test_bench_gloo.py pins
+    these against the oracle's ring.)"""
     tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
     ln = count - off if ln is None else ln
-    i = torch.arange(off, off + ln, device="cuda", dtype=torch.int64)
+    i = torch.arange(off, off + ln, device=device, dtype=torch.int64)
     if op == pgamd.OP_SUM:
         i.remainder_(1000).add_(rank)
         return i.to(tdt)
@@ -437,11 +438,11 @@ def _pattern(count, rank, world, dt, op, off=0, ln=None):
     return torch.where(i == 2, -1, i + 1).to(torch.int32)
 
 
-def _expected_block(count, off, ln, world, dt, op):
+def _expected_block(count, off, ln, world, dt, op, device="cuda"):
     tdt = torch.int32 if dt == pgamd.DT_INT32 else torch.float64
     acc = None
     for q in range(world):
-        v = _pattern(count, q, world, dt, op, off, ln).to(torch.float64 if dt == pgamd.DT_DOUBLE else torch.int64)
+        v = _pattern(count, q, world, dt, op, off, ln, device).to(torch.float64 if dt == pgamd.DT_DOUBLE else torch.int64)
         acc = v if acc is None else (acc + v if op == pgamd.OP_SUM else acc * v)
     if dt == pgamd.DT_INT32:
         acc = ((acc + 2**31) % 2**32 - 2**31)
