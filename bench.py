@@ -65,9 +65,13 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
-    ap.add_argument("--transports", default="rccl,xgmi,xgmi_push",
-                    help="ring-leg transports, comma separated (rccl first: the north-star P2P ring; "
-                         "xgmi_push = PG_TRANSPORT=xgmi with PG_XGMI_MODE=push, timed call only)")
+    ap.add_argument("--transports", default="xgmi,xgmi_push,rccl",
+                    help="ring-leg transports, comma separated (rccl last, so a stalled RCCL leg cannot take "
+                         "the tested xgmi rows with it; xgmi_push = PG_TRANSPORT=xgmi with PG_XGMI_MODE=push, "
+                         "timed call only)")
+    ap.add_argument("--ring-div", type=int, default=1,
+                    help="divide the ring-leg element counts (one-GPU rehearsals over RCCL's socket transport "
+                         "only; the driver's runs keep the BASELINE shapes)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
@@ -82,6 +86,13 @@ def dist_setup(args):
     if os.environ.get("PG_BENCH_ONE_GPU") == "1":   # rehearsal of the N>1 path on a 1-GPU box
         local = 0
         os.environ["PG_DEVICE"] = "0"
+        # RCCL refuses two ranks on one device (its check compares host hash and
+        # bus id): a host id per rank makes it treat the ranks as separate nodes,
+        # so the rccl leg and the RCCL-native cross-check run over its socket
+        # transport on loopback (tests/test_rccl_gpu.py)
+        os.environ["NCCL_HOSTID"] = f"pg-bench-rehearsal-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -532,6 +543,10 @@ def _phases(h, rank, world):
     out = {k: round(max_over_ranks(float(st[k]), world), 1) for k in keys}
     out["bytes_recv_per_rank"] = int(st["bytes_recv"])
     out["zero_copy"] = bool(st["zero_copy"])
+    # an xgmi call whose peer input failed to map is redone with the slot copy:
+    # correct, but it must show up in the record, not only as a slower number
+    out["redone"] = sum_over_ranks(float(st["retried"]), world) > 0
+    out["calls_redone_total"] = int(sum_over_ranks(float(st["calls_redone"]), world))
     t = out["kernel_us"] or out["ring_us"]
     out["recv_gbs_per_rank"] = round(st["bytes_recv"] / t / 1e3, 1) if t else None
     return out
@@ -595,6 +610,9 @@ def ring_leg(lib, args, rank, world, transport, sink):
         dt, count, cfg = pgamd.DT_DOUBLE, 1 << 29, "config4: 8-GPU ring, double sum, 4 GiB/rank"
     else:
         dt, count, cfg = pgamd.DT_DOUBLE, 1 << 27, f"{world}-GPU ring, double sum, 1 GiB/rank"
+    if args.ring_div > 1:
+        count //= args.ring_div
+        cfg += f" / {args.ring_div} (rehearsal size)"
     es = pgamd.ELEM_SIZE[dt]
     hosts = " ".join(["127.0.0.1"] * world).encode()
     os.environ["PG_RANK"] = str(rank)
@@ -613,6 +631,9 @@ def ring_leg(lib, args, rank, world, transport, sink):
             "rccl": "RCCL P2P ring over xGMI",
             "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order",
             "xgmi_push": "each block written to its owner over xGMI (HIP IPC), folded locally in ring order"}[transport]}
+        if os.environ.get("PG_BENCH_ONE_GPU") == "1":
+            res["rehearsal"] = ("all ranks share one GPU; rccl runs over RCCL's socket transport on loopback "
+                                "(NCCL_HOSTID per rank), xgmi's links are the one device's HBM: rates are not a node's")
         sink[transport] = res          # visible to the watchdog's print while the leg runs
         x = _pattern(count, rank, world, dt, pgamd.OP_SUM)
         off, ln = pgamd.block_range(count, world, rank)
@@ -645,14 +666,11 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     res[key] = _ring_variant(lib, rank, world, x, out, count, dt, nr, port_off)
                 except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
                     res[key] = {"error": f"{type(e).__name__}: {e}"}
-        if os.environ.get("PG_BENCH_ONE_GPU") == "1":
-            res["rccl_native"] = "skipped: ranks share one GPU (RCCL refuses duplicate devices)"
-        else:
-            progress(rank, f"  {transport}: RCCL-native cross-check")
-            try:
-                res["rccl_native"] = native_crosscheck(lib, h, rank, world, x, dt)
-            except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
-                res["rccl_native"] = {"error": f"{type(e).__name__}: {e}"}
+        progress(rank, f"  {transport}: RCCL-native cross-check")
+        try:
+            res["rccl_native"] = native_crosscheck(lib, h, rank, world, x, dt)
+        except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
+            res["rccl_native"] = {"error": f"{type(e).__name__}: {e}"}
         # host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)
         progress(rank, f"  {transport}: host-buffer reduce-scatter")
         xh = x.cpu().numpy()
@@ -816,7 +834,10 @@ def main():
                 if txt is None:
                     txt = json.dumps({k: v for k, v in line.items() if k != "ring"})
                 print(txt, flush=True)
-            os._exit(0)
+            # a stalled ring is a failed run, whatever was printed: every rank
+            # exits non-zero so the driver never records it as clean
+            print(f"[bench r{rank}] ring watchdog expired after {args.ring_timeout} s", file=sys.stderr, flush=True)
+            os._exit(3)
 
         dog = threading.Timer(args.ring_timeout, _expire)
         dog.daemon = True

@@ -20,8 +20,10 @@
 extern "C" {
 #endif
 
-/* struct pg.transport values.  Selected with PG_TRANSPORT=rccl|xgmi|loopback. */
-#define PG_TRANSPORT_RCCL     0  /* one process per GPU, RCCL P2P over xGMI (default) */
+/* struct pg.transport values.  Selected with PG_TRANSPORT=rccl|xgmi|loopback;
+ * unset: XGMI when every server-list entry names the same host and W <= 16,
+ * else RCCL. */
+#define PG_TRANSPORT_RCCL     0  /* one process per GPU, RCCL P2P ring (xGMI on a node) */
 #define PG_TRANSPORT_LOOPBACK 1  /* one process, the reference's single-process mock
                                     schedule (src/pg.c:161-179, :264-321) run on the
                                     GPU kernel: results equal the reference's own   */
@@ -148,6 +150,7 @@ struct pg_stats {
   double kernel_us;      /* fold / gather launch + completion               */
   int32_t zero_copy;     /* xgmi: 1 = peers read this call's inputs in place */
   int32_t retried;       /* xgmi: 1 = redone with the slot copy (a peer input failed to map) */
+  int64_t calls_redone;  /* xgmi: calls redone that way on this handle so far (cumulative) */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

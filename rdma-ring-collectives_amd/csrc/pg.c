@@ -277,6 +277,18 @@ static void pg_defaults(struct pg *pg) {
   pg_apply_env(pg);                 /* env after defaults: env wins */
 }
 
+/* Without PG_TRANSPORT: the xgmi transport when every rank is on this node
+ * (every entry of the server list names the same host) and W <= 16 -- it is
+ * the one exercised with real processes (tests/test_xgmi_gpu.py) and it pulls
+ * over all of a GPU's links at once -- else the RCCL ring, which also crosses
+ * nodes.  Both give the same bits (ring fold order). */
+int pg_default_transport(const struct pg *pg) {
+  if (pg->world_size > 16) return PG_TRANSPORT_RCCL;
+  for (int i = 1; i < pg->world_size; ++i)
+    if (strcmp(pg->hosts[i], pg->hosts[0]) != 0) return PG_TRANSPORT_RCCL;
+  return PG_TRANSPORT_XGMI;
+}
+
 int connect_process_group(const char *serverlist, void **out_handle) {
   if (!serverlist || !out_handle) { pg_set_error("connect_process_group: NULL argument"); return -1; }
   struct pg *pg = (struct pg *)calloc(1, sizeof(*pg));
@@ -290,7 +302,8 @@ int connect_process_group(const char *serverlist, void **out_handle) {
   if (pg->world_size == 1) pg->transport = PG_TRANSPORT_SELF;
   else if (tr && strcmp(tr, "loopback") == 0) pg->transport = PG_TRANSPORT_LOOPBACK;
   else if (tr && strcmp(tr, "xgmi") == 0) pg->transport = PG_TRANSPORT_XGMI;
-  else if (!tr || !*tr || strcmp(tr, "rccl") == 0) pg->transport = PG_TRANSPORT_RCCL;
+  else if (tr && strcmp(tr, "rccl") == 0) pg->transport = PG_TRANSPORT_RCCL;
+  else if (!tr || !*tr) pg->transport = pg_default_transport(pg);
   else { pg_set_error("PG_TRANSPORT=%s: expected rccl, xgmi or loopback", tr); goto fail; }
 
   if (pg_impl_create(pg)) goto fail;
@@ -338,7 +351,9 @@ int pg_close(void *pg_handle) {
 int pg_get_stats(void *pg_handle, struct pg_stats *out) {
   struct pg *pg = (struct pg *)pg_handle;
   if (!pg || !pg->impl || !out) return -1;
-  *out = ((struct pg_impl *)pg->impl)->stats;
+  const struct pg_impl *im = (const struct pg_impl *)pg->impl;
+  *out = im->stats;
+  out->calls_redone = im->calls_redone;
   return 0;
 }
 

@@ -75,6 +75,7 @@ struct pg_impl {
   struct pg_step *steps; int steps_cap;
   int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */
   struct pg_stats stats;
+  int64_t calls_redone;       /* cumulative: xgmi calls redone with the slot copy */
 };
 
 /* pg.c */
@@ -89,6 +90,7 @@ size_t pg_elem_size(int dt);
 int pg_is_device_ptr(const void *p);                      /* HIP device/managed memory? */
 int pg_ranges_overlap(const void *a, size_t na, const void *b, size_t nb);
 int pg_timed_copy(void *dst, const void *src, size_t bytes, double *acc_us);  /* any direction */
+int pg_default_transport(const struct pg *pg);            /* no PG_TRANSPORT: xgmi on one node, else rccl */
 
 /* pg_eager.c: one group + one launch for messages <= eager_max (P2P transports) */
 int pg_eager_applies(const struct pg *pg, int count, int dt);

@@ -74,7 +74,6 @@ struct xgmi_ctx {
   int force_copy;               /* this call: no zero-copy (the retry after a failed import) */
   long fail_import_at;          /* test hook PG_XGMI_FAIL_IMPORT=n: the n-th import fails */
   long imports;                 /* imports attempted so far (for the hook)   */
-  long retries;                 /* calls redone with the slot copy            */
   hipIpcMemHandle_t exp_h;      /* last export of a caller allocation       */
   unsigned long long exp_bid;
   void *exp_base;
@@ -253,6 +252,13 @@ int pg_xport_xgmi_init(struct pg *pg) {
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
   const char *nb = getenv("PG_NO_SHM_BARRIER");
   if (!(nb && *nb == '1') && pg_shm_open(pg, im->boot_fds, &x->bar)) return -1;
+  /* push mode publishes its per-call flags in the shm page's descriptor table:
+   * without the page (PG_NO_SHM_BARRIER=1, or shm_open/mmap failed somewhere --
+   * pg_shm_open falls back on every rank together) every rank reads instead */
+  if (x->push && !x->bar) {
+    pg_trace(pg, "xgmi: PG_XGMI_MODE=push needs the shared-memory page; using the read path");
+    x->push = 0;
+  }
   return barrier(pg);
 }
 
@@ -821,8 +827,8 @@ static int xgmi_retry(struct pg *pg, int first) {
   struct xgmi_ctx *x = ctx_of(pg);
   if (first != 1) return first;
   x->force_copy = 1;
-  x->retries++;
   ((struct pg_impl *)pg->impl)->stats.retried = 1;
+  ((struct pg_impl *)pg->impl)->calls_redone++;
   pg_trace(pg, "xgmi: a peer's input could not be mapped; redoing the call with the slot copy");
   return 0;
 }

@@ -56,6 +56,7 @@ class PgStats(ctypes.Structure):
         ("bytes_sent", ctypes.c_int64), ("bytes_recv", ctypes.c_int64),
         ("sync_us", ctypes.c_double), ("copy_us", ctypes.c_double), ("barrier_us", ctypes.c_double),
         ("kernel_us", ctypes.c_double), ("zero_copy", ctypes.c_int32), ("retried", ctypes.c_int32),
+        ("calls_redone", ctypes.c_int64),
     ]
 
 

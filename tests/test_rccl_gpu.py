@@ -1,0 +1,188 @@
+"""PG_TRANSPORT=rccl -- the RCCL point-to-point ring (csrc/pg_xport_rccl.c, the
+replacement of the reference's RC-QP ring, src/RDMA_api.c:93-309 and
+src/pg_net.c:721-783, at the hop sites src/pg.c:287,317) -- with REAL separate
+processes on the one GPU of the test box.
+
+RCCL refuses two ranks on one device ("Duplicate GPU detected"), and that check
+compares (host hash, bus id).  Giving every rank its own NCCL_HOSTID makes RCCL
+treat the ranks as separate nodes, so the communicator comes up and every hop
+travels over RCCL's socket network transport on loopback instead of xGMI.  The
+rates are meaningless; what runs is exactly our path: the unique-id relay, the
+communicator, ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd per batch
+(both rings of a W=2 ring target the same peer inside one group), the recv
+events that gate the reduce stream, and the red events that gate forwarding.
+Every rank checks its output bit for bit against the oracle's ring simulator.
+
+Without the NCCL_HOSTID split the same launch must fail cleanly: both ranks get
+-1 from connect_process_group, neither hangs.
+"""
+import os
+import pathlib
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+CASES = [  # coll, dt, op, count, on_dev, in_place
+    ("rs", 1, 0, 1000, True, False), ("rs", 0, 1, 4099, False, False), ("rs", 1, 1, 1, True, False),
+    ("rs", 0, 0, 0, True, False), ("rs", 1, 0, (1 << 20) + 3, True, False),
+    ("ag", 1, 0, 257, True, False), ("ag", 0, 0, 64, False, False), ("ag", 1, 0, 33, True, True),
+    ("ag", 1, 0, 300001, True, False),
+    ("ar", 1, 0, 100003, True, False), ("ar", 0, 1, 999, False, False), ("ar", 1, 1, 4096, True, True),
+    ("ar", 0, 0, 7, False, True), ("ar", 1, 0, 300001, True, False), ("ar", 0, 1, 524288, False, True),
+    # BASELINE config 1 at its exact shape: int32 sum, count 1,048,576 (reference src/pg.c:264-291)
+    ("rs", 0, 0, 1 << 20, True, False), ("ar", 0, 0, 1 << 20, True, False),
+    ("rs", 0, 0, 1 << 20, False, False), ("ar", 0, 0, 1 << 20, True, True),
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rccl_env(rank, port, split_hosts):
+    env = dict(PG_TRANSPORT="rccl", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+               PG_CONNECT_TIMEOUT_MS="60000", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    if split_hosts:
+        env["NCCL_HOSTID"] = f"pg-rccl-test-{port}-rank{rank}"
+    return env
+
+
+def _worker(rank, world, port, q, rings, chunk_bytes, inflight, cases):
+    os.environ.update(_rccl_env(rank, port, True), PG_RINGS=str(rings), PG_CHUNK_BYTES=str(chunk_bytes),
+                      PG_INFLIGHT=str(inflight))
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        hosts = " ".join(["127.0.0.1"] * world).encode()
+        if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
+            q.put((rank, ["connect: " + pgamd.last_error()]))
+            return
+        hd = pgamd.head(h)
+        assert (hd.rank, hd.world_size, hd.transport) == (rank, world, pgamd.PG_TRANSPORT_RCCL)
+        assert (hd.chunk_bytes, hd.inflight) == (chunk_bytes, inflight)
+        NP = {0: np.int32, 1: np.float64}
+        for i, (coll, dt, op, count, on_dev, in_place) in enumerate(cases):
+            xs = [orc.fill(count, dt, op, 900 + 17 * i + r) for r in range(world)]
+            if coll == "rs":
+                want = orc.ring_reduce_scatter(xs, dt, op, rings)[rank]
+                recv = np.zeros(max(want.size, 1), NP[dt])
+            elif coll == "ag":
+                want = orc.ring_all_gather(xs, dt)[rank]
+                recv = np.zeros(count * world, NP[dt])
+                if in_place:
+                    recv[rank * count:(rank + 1) * count] = xs[rank]
+            else:
+                want = orc.ring_all_reduce(xs, dt, op, rings)[rank]
+                recv = xs[rank].copy() if in_place else np.zeros(count, NP[dt])
+            send = xs[rank] if xs[rank].size else np.zeros(1, NP[dt])
+            if on_dev:
+                S = torch.from_numpy(send.copy()).cuda()
+                R = torch.from_numpy(recv.copy() if recv.size else np.zeros(1, NP[dt])).cuda()
+                sp, rp = S.data_ptr(), R.data_ptr()
+            else:
+                S, R = send.copy(), recv.copy() if recv.size else np.zeros(1, NP[dt])
+                sp, rp = S.ctypes.data, R.ctypes.data
+            if coll == "rs":
+                rc = lib.pg_reduce_scatter(sp, rp, count, dt, op, h)
+            elif coll == "ag":
+                rc = lib.pg_all_gather(None if in_place else sp, rp, count, dt, h)
+            else:
+                rc = lib.pg_all_reduce(rp if in_place else sp, rp, count, dt, op, h)
+            if rc != 0:
+                fails.append((i, "rc", pgamd.last_error()))
+                break
+            got = R.cpu().numpy() if on_dev else R
+            if got[:want.size].tobytes() != want.tobytes():
+                fails.append((i, coll, dt, op, count, on_dev, in_place))
+        lib.pg_close(h)
+    except Exception as e:  # report, never hang the parent
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+def _run(world, target, args_of, timeout=300):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args_of(r)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return results, procs
+
+
+@pytest.mark.parametrize("world,rings,chunk_bytes,inflight", [
+    (2, 2, 4 << 20, 4), (2, 1, 1 << 16, 2), (3, 2, 1 << 18, 4), (4, 4, 1 << 16, 3), (4, 1, 4 << 20, 1)])
+def test_rccl_ring_multiprocess(gpu, world, rings, chunk_bytes, inflight):
+    """The RCCL ring at W = 2, 3, 4 with 1, 2 and 4 rings, small and default
+    segments, against the oracle ring -- every collective form, host and device
+    buffers, in place, the eager one-shot sizes and config 1's exact shape."""
+    cases = CASES if world == 2 else [c for c in CASES if c[3] != 1 << 20]
+    results, procs = _run(world, _worker, lambda r: (rings, chunk_bytes, inflight, cases))
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def _dup_worker(rank, world, port, q):
+    os.environ.update(_rccl_env(rank, port, False))
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    try:
+        import ctypes
+        import time
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        t0 = time.monotonic()
+        rc = lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h))
+        took = time.monotonic() - t0
+        err = pgamd.last_error()
+        if rc == 0:
+            lib.pg_close(h)
+        q.put((rank, (rc, took, err)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, ("exception", repr(e))))
+
+
+def test_rccl_duplicate_device_refused_cleanly(gpu):
+    """Two ranks on one device with one host id: RCCL refuses the communicator,
+    and connect_process_group returns -1 on BOTH ranks (no rank hangs waiting
+    for the other) well inside PG_CONNECT_TIMEOUT_MS."""
+    results, procs = _run(2, _dup_worker, lambda r: (), timeout=180)
+    for rank, res in results:
+        assert res[0] == -1, (rank, res)
+        assert res[1] < 60.0, (rank, res)
+        assert "Duplicate" in res[2] or "invalid usage" in res[2].lower() or "ncclCommInitRank" in res[2], (rank, res)
+    assert all(p.exitcode == 0 for p in procs)

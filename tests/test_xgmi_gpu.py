@@ -35,10 +35,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2, mode="read"):
+def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2, mode="read", extra_env=None):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
                       PG_CONNECT_TIMEOUT_MS="120000", PG_ONESHOT_MAX=str(oneshot_max), PG_XGMI_ZERO_COPY=zero_copy,
                       PG_RINGS=str(rings), PG_XGMI_MODE=mode, PG_BARRIER_TIMEOUT_MS="60000")
+    for k, v in (extra_env or {}).items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -133,6 +138,44 @@ def test_xgmi_multiprocess(gpu, world, oneshot_max, zero_copy, rings, mode):
     for rank, fails in results:
         assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _run_workers(world, args, timeout=420):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_push_without_shm_page_reads(gpu, world):
+    """PG_XGMI_MODE=push with PG_NO_SHM_BARRIER=1: push keeps its per-call
+    flags in the shared-memory page, so without it every rank takes the read
+    path (TCP barrier) instead of dereferencing a missing page.  All cases
+    against the oracle."""
+    _run_workers(world, (1 << 20, "1", 2, "push", {"PG_NO_SHM_BARRIER": "1"}))
+
+
+def test_default_transport_is_xgmi_on_one_node(gpu):
+    """No PG_TRANSPORT, every server-list entry the same host, W <= 16: the
+    xgmi transport (pg_default_transport); the worker asserts the handle's
+    transport and runs every case against the oracle."""
+    _run_workers(2, (1 << 20, "1", 2, "read", {"PG_TRANSPORT": None}))
 
 
 def _grow_worker(rank, world, port, q):
