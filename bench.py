@@ -203,7 +203,8 @@ def kernel_leg(lib, args, rank, world):
     return t1 - t0, region_mean_ms, stamped
 
 
-SWEEP_BYTES = (64 << 20, 128 << 20, 256 << 20, 512 << 20, 1 << 30)   # per operand, north_star: >= 64 MiB
+# per operand: the in-ring launch sizes (4-32 MiB: PG_CHUNK_BYTES x PG_INFLIGHT) and north_star's >= 64 MiB
+SWEEP_BYTES = (4 << 20, 16 << 20, 32 << 20, 64 << 20, 128 << 20, 256 << 20, 512 << 20, 1 << 30)
 SWEEP_POOL = 4 << 30
 
 
@@ -265,17 +266,71 @@ def size_leg(lib, rank, world, reps=20):
             rows.append(["f64" if dt == pgamd.DT_DOUBLE else "i32", "sum" if op == pgamd.OP_SUM else "prod",
                          size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4),
                          round(sms * 1e3, 2), round(sgbs / HBM_PEAK_GBS, 4)])
+    batches = ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     lib.pgk_event_destroy(stamp[0])
     lib.pgk_event_destroy(stamp[1])
     del pool
     torch.cuda.empty_cache()
     return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
-                        "stamped_frac"], "rows": rows,
+                        "stamped_frac"], "rows": rows, "ring_batches": batches,
             "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
                       "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
                       "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
                       "times it), slowest rank; GB/s and frac count 3 x bytes_per_operand (read dst, read src, "
                       "write dst) against 8000 GB/s"}
+
+
+def ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps):
+    """What one reduce launch of the ring executor costs: a batch carries
+    PG_INFLIGHT segments of PG_CHUNK_BYTES for each of PG_RINGS rings, and
+    pg_exec.c reduces all of them with ONE pgk_reduce_ranges launch (each ring's
+    segments are contiguous; different rings work in different blocks).  Timed
+    here alone, on dst/src ranges 64 MiB apart in the 4 GiB pool, rotating, so
+    every launch streams from HBM.  double sum."""
+    import itertools
+    rows = []
+    dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
+    VP, SZ = ctypes.c_void_p, ctypes.c_size_t
+    for chunk, inflight, rings in ((4 << 20, 4, 2), (1 << 20, 4, 2), (16 << 20, 4, 2), (4 << 20, 4, 1),
+                                   (4 << 20, 4, 4), (8 << 20, 4, 2), (4 << 20, 8, 2), (64 << 10, 4, 2)):
+        rng = chunk * inflight                    # bytes per ring per launch, per operand
+        stride = 64 << 20                         # one ring's run per 64 MiB "block"
+        slots = (SWEEP_POOL // (2 * stride)) // rings
+
+        def launch(i, ev=(None, None)):
+            outs, bs, ns = (VP * rings)(), (VP * rings)(), (SZ * rings)()
+            for g in range(rings):
+                d = base + 2 * stride * ((i % slots) * rings + g)
+                outs[g], bs[g], ns[g] = d, d + stride, rng // 8
+            if lib.pgk_reduce_ranges(outs, outs, bs, ns, rings, dt, op, sh, ev[0], ev[1]) != 0:
+                raise RuntimeError(pgamd.last_error())
+
+        for i in range(4):
+            launch(i)
+        torch.cuda.synchronize()
+        barrier(world)
+        e0.record(torch.cuda.current_stream())
+        for i in range(reps):
+            launch(i)
+        e1.record(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+        st = []
+        for i in range(8):
+            launch(i, stamp)
+            torch.cuda.synchronize()
+            v = ctypes.c_float()
+            pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
+            st.append(v.value)
+        sms = max_over_ranks(float(np.median(st)), world)
+        traffic = 3 * rng * rings
+        rows.append([chunk, inflight, rings, rng * rings, round(ms * 1e3, 2),
+                     round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), round(sms * 1e3, 2),
+                     round(traffic / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
+    return {"columns": ["chunk_bytes", "inflight", "rings", "bytes_per_operand", "kernel_us", "frac", "stamped_us",
+                        "stamped_frac"], "rows": rows,
+            "note": "one pgk_reduce_ranges launch = one executor batch (rings ranges of chunk_bytes x inflight), "
+                    "double sum; first row = the library defaults"}
 
 
 def cpu_baseline(args):
@@ -552,6 +607,32 @@ def _phases(h, rank, world):
     return out
 
 
+def _in_ring_reduce(lib, h, x, out, count, dt, rank, world):
+    """The reduce launches inside the ring, measured: one more reduce-scatter
+    with PG_KERNEL_TIMING=1, which stamps every executor launch with its own
+    kernel begin/end (pg_exec.c); per rank, GB/s = 3 x reduced bytes / summed
+    kernel time.  Untimed call: stamping costs a few us per launch."""
+    os.environ["PG_KERNEL_TIMING"] = "1"
+    try:
+        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, pgamd.OP_SUM, h),
+                    "ring RS (kernel-stamped)")
+    finally:
+        os.environ.pop("PG_KERNEL_TIMING", None)
+    st = pgamd.stats(h)
+    us = float(st["red_kernel_us"])
+    moved = 3 * int(st["reduce_elems"]) * pgamd.ELEM_SIZE[dt]
+    gbs = moved / us / 1e3 if us > 0 else 0.0
+    per = gather_over_ranks(gbs, rank, world)
+    launches = int(st["reduce_launches"])
+    return {"launches_per_rank": launches, "kernel_us_per_rank": round(max_over_ranks(us, world), 1),
+            "bytes_per_launch": int(moved / max(launches, 1)),
+            "gbs_per_rank": {"min": round(min(per), 1), "median": round(float(np.median(per)), 1),
+                             "max": round(max(per), 1)},
+            "frac_min": round(min(per) / HBM_PEAK_GBS, 4),
+            "timing": "PG_KERNEL_TIMING=1: each pgk_reduce_ranges launch kernel-stamped; 3 x reduced bytes / "
+                      "summed kernel time, one untimed reduce-scatter"}
+
+
 def _ring_variant(lib, rank, world, x, out, count, dt, rings, port_off):
     """The same timed reduce-scatter with PG_RINGS=`rings` (a second handle and
     RCCL communicator): rings = 1 shows what the counter-rotating second ring
@@ -647,6 +728,8 @@ def ring_leg(lib, args, rank, world, transport, sink):
         wall = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, args.ring_steps, world)
         payload = count * es                       # per rank
         res["last_call_phases"] = _phases(h, rank, world)
+        if not transport.startswith("xgmi"):       # xgmi folds in its own kernels, no executor launches
+            res["in_ring_reduce"] = _in_ring_reduce(lib, h, x, out, count, dt, rank, world)
         res.update({"ms_per_reduce_scatter": round(wall * 1e3, 3),
                     "algbw_gibs": round(payload / wall / GIB, 2),
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),

@@ -67,8 +67,11 @@ PG_API int pg_ring_offset(int world, int rings, int part);
  * (rank + send_peer) and receive `recv_bytes` from rank (rank + recv_peer),
  * mod world (d / -d of the step's ring: the clockwise ring sends right and
  * receives from the left, the counter-clockwise ring the opposite); then (on the reduce stream,
- * after the receive) red_dst[i] = red_dst[i] op red_src[i] for i < red_elems.
- * Offsets/lengths in bytes except red_elems. */
+ * after the receive) red_dst[i] = red_dst[i] op red_src[i] for i < red_elems,
+ * or, with red_rev, red_dst[i] = red_src[i] op red_dst[i]: the arrival is
+ * always the left operand (the ring order), which matters for the NaN payload
+ * a sum or product of two NaNs returns.  Offsets/lengths in bytes except
+ * red_elems. */
 struct pg_step {
   int32_t round;       /* ring round k, 0 .. world-2                          */
   int32_t batch;       /* steps with equal batch share one transport group    */
@@ -80,6 +83,8 @@ struct pg_step {
   int64_t send_off, send_bytes;
   int64_t recv_off, recv_bytes;
   int64_t red_dst_off, red_src_off, red_elems;
+  int32_t red_rev;     /* 1: red_dst = red_src op red_dst (in-place last round) */
+  int32_t reserved;
 };
 
 /* Reduce-scatter plan for one rank.  Clockwise ring: round k sends block
@@ -151,6 +156,8 @@ struct pg_stats {
   int32_t zero_copy;     /* xgmi: 1 = peers read this call's inputs in place */
   int32_t retried;       /* xgmi: 1 = redone with the slot copy (a peer input failed to map) */
   int64_t calls_redone;  /* xgmi: calls redone that way on this handle so far (cumulative) */
+  double red_kernel_us;  /* ring: summed kernel time of the reduce launches, when
+                            PG_KERNEL_TIMING=1 stamps each launch (else 0)   */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

@@ -47,6 +47,16 @@ PG_API int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void
 PG_API int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
                    void *stream);
 
+/* Up to 8 independent ranges in one launch: outs[j][i] = as[j][i] op bs[j][i]
+ * for i < ns[j] (out may equal a or b within a range; ranges must not overlap
+ * each other).  Same numerics as pgk_reduce.  The ring executor reduces every
+ * ring's arrived segments of a batch with one call.  start_event/stop_event
+ * (hipEvent_t as void*, may be NULL) receive the kernel's own begin/end
+ * timestamps as in pgk_reduce_timed; ranges that cannot share one launch
+ * (not 16-byte congruent) are launched one by one, stamped first-to-last. */
+PG_API int pgk_reduce_ranges(void *const *outs, const void *const *as, const void *const *bs, const size_t *ns,
+                             int k, int dt, int op, void *stream, void *start_event, void *stop_event);
+
 /* out[i] = ((srcs[0][i] op srcs[1][i]) op srcs[2][i]) ... op srcs[nsrc-1][i],
  * folded left to right (1 <= nsrc <= 16).  Sources may be peer GPUs' memory
  * mapped through HIP IPC (read over xGMI).  With srcs in ring order this is

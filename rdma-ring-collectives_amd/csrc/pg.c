@@ -108,6 +108,47 @@ int pg_stream_wait(hipStream_t s) {
   return 0;
 }
 
+/* Same bounded spin for an event. */
+static int pg_event_wait(hipEvent_t ev) {
+  static double spin_us = -1.0;
+  if (spin_us < 0) {
+    const char *e = getenv("PG_SPIN_US");
+    spin_us = (e && *e) ? atof(e) : 200.0;
+  }
+  double t0 = spin_us > 0 ? now_us() : 0;
+  while (spin_us > 0) {
+    hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) {
+      pg_set_error("event wait: %s", hipGetErrorString(e));
+      return -1;
+    }
+    if (now_us() - t0 > spin_us) break;
+    __builtin_ia32_pause();
+  }
+  PG_CHECK_HIP(hipEventSynchronize(ev));
+  return 0;
+}
+
+/* Device buffers: the caller's producers are the work it enqueued on the null
+ * stream before the call -- and, through the null stream's implicit
+ * synchronisation, on every blocking stream ("Device
+ * buffers").  The collective must not read its buffers before that work ends.
+ * The ring's streams wait for it on the device (host_wait = 0): nothing blocks
+ * the host, and the first transfer is queued behind the producer.  A transport
+ * whose peers read this rank's buffers once it reaches a host barrier (xgmi)
+ * waits on the host instead (host_wait = 1).  Either way it is narrower than a
+ * hipDeviceSynchronize(): non-blocking streams of the process that the caller
+ * did not order before the call (another thread's work, RCCL's) are not
+ * waited for (tests/test_api_gpu.py::test_device_input_behind_slow_producer). */
+int pg_wait_producers(struct pg_impl *im, int host_wait) {
+  PG_CHECK_HIP(hipEventRecord(im->entry_ev, NULL));
+  if (host_wait) return pg_event_wait(im->entry_ev);
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->entry_ev, 0));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->red, im->entry_ev, 0));
+  return 0;
+}
+
 int pg_ensure(void **buf, size_t *cap, size_t bytes) {
   if (bytes <= *cap && (*buf || bytes == 0)) return 0;
   if (*buf) { hipFree(*buf); *buf = NULL; *cap = 0; }
@@ -228,6 +269,7 @@ int pg_impl_create(struct pg *pg) {
   for (int i = 0; i < PG_RECV_EVENTS; ++i)
     PG_CHECK_HIP(hipEventCreateWithFlags(&im->recv_ev[i], hipEventDisableTiming));
   PG_CHECK_HIP(hipEventCreateWithFlags(&im->join_ev, hipEventDisableTiming));
+  PG_CHECK_HIP(hipEventCreateWithFlags(&im->entry_ev, hipEventDisableTiming));
   PG_CHECK_HIP(hipEventCreate(&im->t0));
   PG_CHECK_HIP(hipEventCreate(&im->t1));
   const char *e = getenv("PG_EAGER_ONESHOT");
@@ -256,6 +298,9 @@ void pg_impl_destroy(struct pg *pg) {
   free(im->round_ev);
   for (int i = 0; i < PG_RECV_EVENTS; ++i) if (im->recv_ev[i]) hipEventDestroy(im->recv_ev[i]);
   if (im->join_ev) hipEventDestroy(im->join_ev);
+  if (im->entry_ev) hipEventDestroy(im->entry_ev);
+  for (int i = 0; i < im->n_kt_ev; ++i) hipEventDestroy(im->kt_ev[i]);
+  free(im->kt_ev);
   if (im->t0) hipEventDestroy(im->t0);
   if (im->t1) hipEventDestroy(im->t1);
   if (im->comm) hipStreamDestroy(im->comm);
@@ -357,7 +402,16 @@ int pg_get_stats(void *pg_handle, struct pg_stats *out) {
   return 0;
 }
 
-static void stats_begin(struct pg_impl *im) { memset(&im->stats, 0, sizeof(im->stats)); }
+/* PG_KERNEL_TIMING=1: every reduce launch of the ring executor carries its own
+ * kernel timestamps (pgk_reduce_ranges start/stop events); the call's summed
+ * kernel time lands in pg_stats.red_kernel_us.  Stamping costs a few us per
+ * launch, so it is for measuring calls, not for timed ones. */
+static void stats_begin(struct pg_impl *im) {
+  memset(&im->stats, 0, sizeof(im->stats));
+  const char *e = getenv("PG_KERNEL_TIMING");
+  im->kt_on = e && *e == '1';
+  im->kt_used = 0;
+}
 
 static int sync_ring(struct pg_impl *im, int timed) {
   if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
@@ -365,6 +419,12 @@ static int sync_ring(struct pg_impl *im, int timed) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
   }
+  for (int u = 0; u < im->kt_used; ++u) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, im->kt_ev[2 * u], im->kt_ev[2 * u + 1]) == hipSuccess)
+      im->stats.red_kernel_us += (double)ms * 1e3;
+  }
+  im->kt_used = 0;
   return 0;
 }
 
@@ -483,7 +543,7 @@ static int ring_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int 
   size_t es = pg_elem_size(dt), boff, blen;
   pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
   int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
-  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());   /* caller's producers */
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
 
   void *src = sendbuf;
   unsigned char up[64];
@@ -545,7 +605,7 @@ static int loopback_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, 
     }
   }
   int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
-  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
   char *s, *d;
   if (sendbuf == recvbuf) {
     if (rd) s = d = (char *)recvbuf;
@@ -620,7 +680,7 @@ static int ring_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)pg->world_size;
   int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
-  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((rd || sd) && pg_wait_producers(im, 0)) return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
@@ -660,7 +720,7 @@ static int loopback_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int 
   int W = pg->world_size, r = pg->rank;
   size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)W;
   int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
-  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((rd || sd) && pg_wait_producers(im, 0)) return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, total) || pg_timed_copy(im->dout, recvbuf, total, &im->stats.h2d_us)) return -1;
@@ -716,7 +776,7 @@ static int ring_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int coun
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, boff, blen;
   pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
   int rd = pg_is_device_ptr(recvbuf), sd = pg_is_device_ptr(sendbuf);
-  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((rd || sd) && pg_wait_producers(im, 0)) return -1;
   char *work = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;

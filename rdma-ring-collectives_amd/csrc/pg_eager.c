@@ -59,7 +59,7 @@ int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int cou
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es, boff, blen;
   pg_block_range(count, W, r, &boff, &blen);
   int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
-  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
   const char *src;
   if (device_input(im, sendbuf, sd, bytes, (const void **)&src)) return -1;
   /* gather area: block r of every rank, one slot per rank; the output goes
@@ -120,7 +120,7 @@ int pg_eager_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, 
   const int W = pg->world_size, r = pg->rank;
   size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)W;
   int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
-  if (rd || sd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((rd || sd) && pg_wait_producers(im, 0)) return -1;
   char *full = (char *)recvbuf;
   if (!rd) {
     if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
@@ -151,7 +151,7 @@ int pg_eager_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, 
   const int W = pg->world_size, r = pg->rank;
   size_t es = pg_elem_size(dt), bytes = (size_t)count * es;
   int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
-  if (sd || rd) PG_CHECK_HIP(hipDeviceSynchronize());
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
   const char *src;
   if (device_input(im, sendbuf, sd, bytes, (const void **)&src)) return -1;
   /* every peer's whole input, plus an output slot when recvbuf is host

@@ -65,6 +65,52 @@ static int ensure_round_events(struct pg_impl *im, int need) {
   return 0;
 }
 
+/* The reduce launches of one batch: up to PG_RED_RANGES ranges per
+ * pgk_reduce_ranges call. */
+#define PG_RED_RANGES 8
+struct red_batch {
+  void *out[PG_RED_RANGES];
+  const void *a[PG_RED_RANGES], *b[PG_RED_RANGES];
+  size_t n[PG_RED_RANGES];
+  int k;
+};
+
+/* Next start/stop event pair for a stamped launch (PG_KERNEL_TIMING=1). */
+static int kt_pair(struct pg_impl *im, void **t0, void **t1) {
+  if (2 * (im->kt_used + 1) > im->n_kt_ev) {
+    int cap = im->n_kt_ev ? 2 * im->n_kt_ev : 64;
+    hipEvent_t *ev = (hipEvent_t *)realloc(im->kt_ev, sizeof(hipEvent_t) * (size_t)cap);
+    if (!ev) { pg_set_error("pg_exec: out of host memory"); return -1; }
+    im->kt_ev = ev;
+    for (int i = im->n_kt_ev; i < cap; ++i) {
+      hipError_t e = hipEventCreate(&im->kt_ev[i]);
+      if (e != hipSuccess) {
+        im->n_kt_ev = i & ~1;
+        pg_set_error("pg_exec: hipEventCreate: %s", hipGetErrorString(e));
+        return -1;
+      }
+    }
+    im->n_kt_ev = cap;
+  }
+  *t0 = (void *)im->kt_ev[2 * im->kt_used];
+  *t1 = (void *)im->kt_ev[2 * im->kt_used + 1];
+  im->kt_used++;
+  return 0;
+}
+
+static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op) {
+  if (!rb->k) return 0;
+  void *t0 = NULL, *t1 = NULL;
+  if (im->kt_on && kt_pair(im, &t0, &t1)) return -1;
+  if (pgk_reduce_ranges(rb->out, rb->a, rb->b, rb->n, rb->k, dt, op, (void *)im->red, t0, t1)) {
+    pg_set_error("pg_exec: %s", pgk_last_error());
+    return -1;
+  }
+  im->stats.reduce_launches += 1;
+  rb->k = 0;
+  return 0;
+}
+
 int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
                  void *const bufs[5], int dt, int op, pg_round_hook hook, void *hook_ctx) {
   if (n <= 0) {
@@ -122,33 +168,39 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
       hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
       PG_CHECK_HIP(hipEventRecord(rev, im->comm));
       PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-      /* one launch per run of segments that are contiguous in both operands
-       * (a batch's segments are neighbours in the same block) */
+      /* runs of segments contiguous in both operands (a batch's segments of
+       * one ring are neighbours in the same block), and every run of the batch
+       * -- one per ring -- in one pgk_reduce_ranges launch */
+      struct red_batch rb;
+      rb.k = 0;
       const int64_t es = pg_elem_size(dt);
       int s = i;
       while (s < j) {
         if (!st[s].red_elems) { ++s; continue; }
         int e = s + 1;
         int64_t elems = st[s].red_elems;
-        while (e < j && st[e].red_elems && st[e].red_dst_buf == st[s].red_dst_buf &&
-               st[e].red_src_buf == st[s].red_src_buf &&
+        while (e < j && st[e].red_elems && st[e].red_rev == st[s].red_rev &&
+               st[e].red_dst_buf == st[s].red_dst_buf && st[e].red_src_buf == st[s].red_src_buf &&
                st[e].red_dst_off == st[s].red_dst_off + elems * es &&
                st[e].red_src_off == st[s].red_src_off + elems * es) {
           elems += st[e].red_elems;
           ++e;
         }
-        if (pgk_reduce(at(bufs, st[s].red_dst_buf, st[s].red_dst_off),
-                       at(bufs, st[s].red_src_buf, st[s].red_src_off),
-                       (size_t)elems, dt, op, (void *)im->red)) {
-          pg_set_error("pg_exec: %s", pgk_last_error());
-          return -1;
-        }
-        im->stats.reduce_launches += 1;
+        char *dst = at(bufs, st[s].red_dst_buf, st[s].red_dst_off);
+        const char *src = at(bufs, st[s].red_src_buf, st[s].red_src_off);
+        /* the arrival is the left operand: dst = dst op src, or with red_rev
+         * (the arrival sits in src) dst = src op dst */
+        rb.out[rb.k] = dst;
+        rb.a[rb.k] = st[s].red_rev ? src : dst;
+        rb.b[rb.k] = st[s].red_rev ? dst : src;
+        rb.n[rb.k] = (size_t)elems;
         im->stats.reduce_elems += elems;
-        for (int t = s; t < e; ++t)
-          if (st[t].red_elems) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[t].seg], im->red));
+        if (++rb.k == PG_RED_RANGES && red_flush(im, &rb, dt, op)) return -1;
         s = e;
       }
+      if (red_flush(im, &rb, dt, op)) return -1;
+      for (int t = i; t < j; ++t)
+        if (st[t].red_elems) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[t].seg], im->red));
     }
     ++nb;
     i = j;

@@ -60,6 +60,9 @@ struct pg_impl {
   int n_red_ev;
   hipEvent_t recv_ev[PG_RECV_EVENTS]; /* per batch: its receives landed       */
   hipEvent_t join_ev, t0, t1;
+  hipEvent_t entry_ev;        /* the caller's null-stream work at entry (pg_wait_producers) */
+  hipEvent_t *kt_ev;          /* PG_KERNEL_TIMING=1: start/stop pairs of this call's reduce launches */
+  int n_kt_ev, kt_used, kt_on;
   hipEvent_t *round_ev;       /* per ring round: recorded behind its transfers */
   int n_round_ev;
   int last_round_rec;         /* round whose round_ev was recorded last, -1: none */
@@ -83,6 +86,7 @@ void pg_set_error(const char *fmt, ...);
 void pg_trace(const struct pg *pg, const char *fmt, ...);
 int pg_ensure(void **buf, size_t *cap, size_t bytes);   /* hipMalloc-grow */
 int pg_stream_wait(hipStream_t s);                        /* bounded spin, then block */
+int pg_wait_producers(struct pg_impl *im, int host_wait); /* caller's pending null-stream work */
 int pg_copy_parallel(void *dst, const void *src, size_t bytes);  /* host<->device, threaded */
 int pg_impl_create(struct pg *pg);                        /* streams/events */
 void pg_impl_destroy(struct pg *pg);

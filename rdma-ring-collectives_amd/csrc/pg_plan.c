@@ -183,11 +183,12 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
             st.recv_bytes = (int64_t)(len * es);
             st.red_elems = (int64_t)len;
             if (last && out_aliases_src) {
-              /* OUT is block `rank` of SRC: fold the arrival into it in place
-               * (local op incoming == incoming op local bit for bit: + and * are
-               * commutative in IEEE-754 and in two's complement) */
+              /* OUT is block `rank` of SRC: fold the arrival into it in place,
+               * arrival op own like every other round (red_rev): + and * commute
+               * except in the payload of NaN op NaN, which is the left operand's */
               st.red_dst_buf = PG_BUF_OUT; st.red_dst_off = (int64_t)((q->tp + e0) * es);
               st.red_src_buf = stage;      st.red_src_off = stage_off;
+              st.red_rev = 1;
             } else {
               /* arrival op= this rank's own contribution to the block */
               st.red_dst_buf = st.recv_buf; st.red_dst_off = st.recv_off;

@@ -448,7 +448,7 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
   *zero_copy = 0;
   *fail = 0;
   double t0 = us_now();
-  if (in_dev) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  if (in_dev && pg_wait_producers(im, 1)) return -1;        /* peers read it after the barrier */
   double t1 = us_now();
   im->stats.sync_us += t1 - t0;
   if (x->zc && x->bar && bytes) {
@@ -633,7 +633,7 @@ static int push_inputs(struct pg *pg, const char *in, int count, int dt, int can
   const size_t es = pg_elem_size(dt), stride = push_stride(count, W, es);
   *pushed = 0;
   double t0 = us_now();
-  if (can) PG_CHECK_HIP(hipDeviceSynchronize());            /* caller's producers */
+  if (can && pg_wait_producers(im, 1)) return -1;          /* peers read it after the barrier */
   double t1 = us_now();
   im->stats.sync_us += t1 - t0;
   struct xg_desc mine;

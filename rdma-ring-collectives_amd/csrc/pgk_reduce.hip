@@ -60,16 +60,16 @@ __device__ __forceinline__ void st(X* p, X v) {
 // out = a op b over [head elements | nvec 16-B vectors | tail elements].
 // The vector region starts at element `head` and is 16-B aligned in all three
 // pointers; head/tail (< one vector each) are done by the first threads of
-// block 0.  Grid-strided so the host can cap the grid.
+// block 0.  Grid-strided so the host can cap the grid.  `bid` / `nblocks` are
+// this block's index and the block count of the range it works on (the whole
+// grid for k_reduce_vec, one range's share for k_reduce_ranges).
 template <typename T, int OP, bool NT, int kBlock, int kUnroll>
-__global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
-                                                       const T* __restrict__ a,
-                                                       const T* __restrict__ b,
-                                                       unsigned head, size_t nvec,
-                                                       unsigned tail) {
+__device__ __forceinline__ void reduce_vec_body(T* __restrict__ out, const T* __restrict__ a,
+                                                const T* __restrict__ b, unsigned head, size_t nvec,
+                                                unsigned tail, unsigned bid, unsigned nblocks) {
   using V = typename VecOf<T>::type;
   constexpr int W = VecOf<T>::width;
-  if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+  if (bid == 0 && threadIdx.x < head + tail) {
     size_t e = threadIdx.x < head ? threadIdx.x
                                   : head + nvec * W + (threadIdx.x - head);
     out[e] = apply<OP>(a[e], b[e]);
@@ -78,8 +78,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
   const V* __restrict__ va = reinterpret_cast<const V*>(a + head);
   const V* __restrict__ vb = reinterpret_cast<const V*>(b + head);
   const size_t tile = (size_t)kBlock * kUnroll;
-  const size_t stride = (size_t)gridDim.x * tile;
-  size_t i = (size_t)blockIdx.x * tile + threadIdx.x;
+  const size_t stride = (size_t)nblocks * tile;
+  size_t i = (size_t)bid * tile + threadIdx.x;
   // full tiles: no bounds checks, kUnroll independent loads per operand
   for (; i + (kUnroll - 1) * kBlock < nvec; i += stride) {
     V x[kUnroll], y[kUnroll];
@@ -98,6 +98,42 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
       if (j < nvec) st<NT>(vo + j, apply<OP>(ld<NT>(va + j), ld<NT>(vb + j)));
     }
   }
+}
+
+template <typename T, int OP, bool NT, int kBlock, int kUnroll>
+__global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
+                                                       const T* __restrict__ a,
+                                                       const T* __restrict__ b,
+                                                       unsigned head, size_t nvec,
+                                                       unsigned tail) {
+  reduce_vec_body<T, OP, NT, kBlock, kUnroll>(out, a, b, head, nvec, tail, blockIdx.x, gridDim.x);
+}
+
+// Several independent ranges in one launch: range j covers blocks
+// [first[j], first[j+1]) of the grid and computes out[j] = a[j] op b[j] with
+// the same body as k_reduce_vec.  One launch instead of one per range: the
+// ring executor reduces every ring's arrived segments of a batch at once
+// (they lie in different blocks of the buffers), so the launch ramp and tail
+// are paid once per batch, not once per ring.
+constexpr int kMaxRanges = 8;
+template <typename T>
+struct RangeList {
+  T* out[kMaxRanges];
+  const T* a[kMaxRanges];
+  const T* b[kMaxRanges];
+  size_t nvec[kMaxRanges];
+  unsigned head[kMaxRanges];
+  unsigned tail[kMaxRanges];
+  unsigned first[kMaxRanges + 1];
+  int k;
+};
+
+template <typename T, int OP, bool NT, int kBlock, int kUnroll>
+__global__ __launch_bounds__(kBlock) void k_reduce_ranges(RangeList<T> rl) {
+  int r = 0;
+  while (r + 1 < rl.k && blockIdx.x >= rl.first[r + 1]) ++r;
+  reduce_vec_body<T, OP, NT, kBlock, kUnroll>(rl.out[r], rl.a[r], rl.b[r], rl.head[r], rl.nvec[r], rl.tail[r],
+                                               blockIdx.x - rl.first[r], rl.first[r + 1] - rl.first[r]);
 }
 
 // Fallback when the three pointers are not mutually 16-B congruent (e.g. a
@@ -394,6 +430,58 @@ int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, vo
   return 0;
 }
 
+template <typename T, int OP, bool NT, int B, int U>
+void launch_ranges_shape(unsigned grid, const RangeList<T>& rl, hipStream_t s, Timing tm) {
+  hipExtLaunchKernelGGL((k_reduce_ranges<T, OP, NT, B, U>), dim3(grid), dim3(B), 0, s, tm.start, tm.stop, 0, rl);
+}
+
+template <typename T, int OP, bool NT>
+void launch_ranges_nt(int block, int unroll, unsigned grid, const RangeList<T>& rl, hipStream_t s, Timing tm) {
+  switch (block * 16 + unroll) {
+    case 256 * 16 + 2: launch_ranges_shape<T, OP, NT, 256, 2>(grid, rl, s, tm); break;
+    case 256 * 16 + 8: launch_ranges_shape<T, OP, NT, 256, 8>(grid, rl, s, tm); break;
+    case 512 * 16 + 2: launch_ranges_shape<T, OP, NT, 512, 2>(grid, rl, s, tm); break;
+    case 1024 * 16 + 1: launch_ranges_shape<T, OP, NT, 1024, 1>(grid, rl, s, tm); break;
+    default: launch_ranges_shape<T, OP, NT, 256, 4>(grid, rl, s, tm);
+  }
+}
+
+// k ranges, each 16-B congruent (plan_for(...).vec), in one launch; the
+// shape is the one a single launch of the largest range would use, and each
+// range gets the blocks that launch would give it.  Returns hipErrorInvalidValue
+// (nothing launched) when the ranges do not fit one grid.
+template <typename T, int OP>
+hipError_t launch_ranges_t(T* const* outs, const T* const* as, const T* const* bs, const size_t* ns, int k,
+                           hipStream_t s, Timing tm) {
+  RangeList<T> rl{};
+  size_t most = 0;
+  for (int j = 0; j < k; ++j) most = ns[j] > most ? ns[j] : most;
+  int block = 0, unroll = 0;
+  shape_for(most * sizeof(T), &block, &unroll);
+  const size_t tile = (size_t)block * (size_t)unroll, W = 16 / sizeof(T);
+  size_t total = 0;
+  rl.k = k;
+  for (int j = 0; j < k; ++j) {
+    uintptr_t m = (uintptr_t)outs[j] & 15;
+    size_t head = m ? (16 - m) / sizeof(T) : 0;
+    if (head > ns[j]) head = ns[j];
+    rl.out[j] = outs[j];
+    rl.a[j] = as[j];
+    rl.b[j] = bs[j];
+    rl.head[j] = (unsigned)head;
+    rl.nvec[j] = (ns[j] - head) / W;
+    rl.tail[j] = (unsigned)((ns[j] - head) % W);
+    size_t blocks = (rl.nvec[j] + tile - 1) / tile;
+    rl.first[j] = (unsigned)total;
+    total += blocks ? blocks : 1;
+    if (total > grid_cap((unsigned)block)) return hipErrorInvalidValue;
+  }
+  rl.first[k] = (unsigned)total;
+  if (g_nontemporal) launch_ranges_nt<T, OP, true>(block, unroll, (unsigned)total, rl, s, tm);
+  else launch_ranges_nt<T, OP, false>(block, unroll, (unsigned)total, rl, s, tm);
+  return hipGetLastError();
+}
+
 template <typename T, int OP>
 hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s) {
   SrcList<T> sl{};
@@ -544,6 +632,61 @@ int pgk_gather(void* const* dsts, const void* const* srcs, const size_t* bytes, 
   hipLaunchKernelGGL(k_gather, dim3((unsigned)g, (unsigned)m), dim3(kMultiBlock), 0, (hipStream_t)stream, cl);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_reduce_ranges(void* const* outs, const void* const* as, const void* const* bs, const size_t* ns, int k,
+                      int dt, int op, void* stream, void* start_event, void* stop_event) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
+  if (k < 0 || k > kMaxRanges || (k && (!outs || !as || !bs || !ns))) {
+    set_err("pgk: reduce_ranges takes 0 .. %d ranges", kMaxRanges);
+    return -1;
+  }
+  const size_t es = dt == PGK_DT_INT32 ? 4 : 8;
+  void* o[kMaxRanges];
+  const void* a[kMaxRanges];
+  const void* b[kMaxRanges];
+  size_t n[kMaxRanges];
+  int m = 0;
+  bool vec = true;
+  for (int j = 0; j < k; ++j) {
+    if (!ns[j]) continue;
+    if (!outs[j] || !as[j] || !bs[j]) { set_err("pgk: NULL buffer in range %d", j); return -1; }
+    o[m] = outs[j];
+    a[m] = as[j];
+    b[m] = bs[j];
+    n[m] = ns[j];
+    vec = vec && plan_for(o[m], a[m], b[m], n[m], es).vec;
+    ++m;
+  }
+  if (!m) return 0;
+  Timing tm{(hipEvent_t)start_event, (hipEvent_t)stop_event};
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipErrorInvalidValue;
+  if (vec && m > 1) {
+    if (dt == PGK_DT_INT32) {
+      e = op == PGK_OP_SUM
+              ? launch_ranges_t<uint32_t, PGK_OP_SUM>((uint32_t* const*)o, (const uint32_t* const*)a,
+                                                     (const uint32_t* const*)b, n, m, s, tm)
+              : launch_ranges_t<uint32_t, PGK_OP_PROD>((uint32_t* const*)o, (const uint32_t* const*)a,
+                                                      (const uint32_t* const*)b, n, m, s, tm);
+    } else {
+      e = op == PGK_OP_SUM
+              ? launch_ranges_t<double, PGK_OP_SUM>((double* const*)o, (const double* const*)a,
+                                                   (const double* const*)b, n, m, s, tm)
+              : launch_ranges_t<double, PGK_OP_PROD>((double* const*)o, (const double* const*)a,
+                                                    (const double* const*)b, n, m, s, tm);
+    }
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorInvalidValue) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  }
+  // one launch per range (a misaligned range, a single range, or ranges too
+  // large for one grid); the start stamp goes on the first, the stop on the last
+  for (int j = 0; j < m; ++j) {
+    Timing tj{j == 0 ? tm.start : nullptr, j == m - 1 ? tm.stop : nullptr};
+    if (launch(o[j], a[j], b[j], n[j], dt, op, stream, tj)) return -1;
+  }
   return 0;
 }
 

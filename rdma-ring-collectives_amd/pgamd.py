@@ -41,6 +41,7 @@ class PgStep(ctypes.Structure):
         ("recv_off", ctypes.c_int64), ("recv_bytes", ctypes.c_int64),
         ("red_dst_off", ctypes.c_int64), ("red_src_off", ctypes.c_int64),
         ("red_elems", ctypes.c_int64),
+        ("red_rev", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -56,7 +57,7 @@ class PgStats(ctypes.Structure):
         ("bytes_sent", ctypes.c_int64), ("bytes_recv", ctypes.c_int64),
         ("sync_us", ctypes.c_double), ("copy_us", ctypes.c_double), ("barrier_us", ctypes.c_double),
         ("kernel_us", ctypes.c_double), ("zero_copy", ctypes.c_int32), ("retried", ctypes.c_int32),
-        ("calls_redone", ctypes.c_int64),
+        ("calls_redone", ctypes.c_int64), ("red_kernel_us", ctypes.c_double),
     ]
 
 
@@ -97,6 +98,8 @@ _SIGS = {
     # include/pgk.h
     "pgk_reduce": (_I, [_VP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
+    "pgk_reduce_ranges": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ),
+                               _I, _I, _I, _VP, _VP, _VP]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),

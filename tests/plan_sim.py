@@ -19,7 +19,13 @@ import pgamd
 NP = {0: np.int32, 1: np.float64}
 
 
-def np_reduce(dst: np.ndarray, src: np.ndarray, op: int) -> None:
+def np_reduce(dst: np.ndarray, src: np.ndarray, op: int, rev: int = 0) -> None:
+    """dst op= src, or dst = src op dst (rev: a plan step's red_rev)."""
+    if rev:
+        tmp = src.copy()
+        np_reduce(tmp, dst, op)
+        dst[:] = tmp
+        return
     if dst.dtype == np.int32:
         d, s = dst.view(np.uint32), src.view(np.uint32)
         if op == 0:
@@ -89,7 +95,7 @@ def run_plans(plans, bufs_per_rank, dt, op):
                 if s["red_elems"]:
                     d = _view(bufs, s["red_dst_buf"], s["red_dst_off"], s["red_elems"] * es).view(NP[dt])
                     src = _view(bufs, s["red_src_buf"], s["red_src_off"], s["red_elems"] * es).view(NP[dt])
-                    np_reduce(d, src, op)
+                    np_reduce(d, src, op, s.get("red_rev", 0))
             pos[r] += 1
             pending[r] = None
             progress = True

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import pgamd
-from gpu_util import open_local, ptr, to_dev, to_host
+from gpu_util import open_local, ptr, same_bits_nan_aware, to_dev, to_host
 
 pytestmark = pytest.mark.gpu
 NP = {0: np.int32, 1: np.float64}
@@ -376,3 +376,89 @@ def test_ring_random_sim(gpu, lib, oracle):
         case = (i, world, coll, dt, op, count, cb, eager, infl, rings, on_dev)
         for r in range(world):
             assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (case, r)
+
+
+@pytest.mark.parametrize("rings", [1, 2])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_nan_payloads_all_reduce_matches_reduce_scatter(gpu, lib, oracle, world, rings):
+    """Every rank's input holds NaNs with its own payload at the same
+    positions.  A sum or product of two NaNs returns the left operand's
+    payload, so the in-place last round of the all-reduce must keep the ring's
+    arrival-first order (plan step red_rev): all-reduce block r == reduce-scatter
+    block r bit for bit, NaN payloads included, in place and out of place."""
+    torch = gpu
+    count = 4099
+    for op in (0, 1):
+        xs = []
+        for r in range(world):
+            x = oracle.fill(count, 1, op, 9100 + r)
+            bits = x.view(np.uint64)
+            idx = np.arange(0, count, 7)
+            bits[idx] = np.uint64(0x7FF8000000000000) | np.uint64((r + 1) << 20) | idx.astype(np.uint64)
+            xs.append(x)
+        rs = sim(lib, torch, pgamd.PG_COLL_REDUCE_SCATTER, xs, [np.zeros(count, np.float64) for _ in xs],
+                 count, 1, op, 1 << 12, 0, 2, True, rings)
+        ar = sim(lib, torch, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, np.float64) for _ in xs],
+                 count, 1, op, 1 << 12, 0, 2, True, rings)
+        R = [to_dev(torch, x) for x in xs]
+        ps = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
+        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, 1, op, 1 << 12, 0, 2, rings) == 0
+        ar_in = [to_host(torch, t) for t in R]
+        want = oracle.ring_reduce_scatter(xs, 1, op, rings)
+        for r in range(world):
+            off, ln = pgamd.block_range(count, world, r)
+            assert np.isnan(want[r]).sum() >= ln // 7          # the NaN positions survive the fold
+            assert same_bits_nan_aware(rs[r][:ln], want[r]), (world, rings, op, r)
+            assert ar[r][off:off + ln].tobytes() == rs[r][:ln].tobytes(), (world, rings, op, r, "out of place")
+            assert ar_in[r][off:off + ln].tobytes() == rs[r][:ln].tobytes(), (world, rings, op, r, "in place")
+
+
+def test_device_input_behind_slow_producer(gpu, lib, oracle):
+    """The entry wait (pg_wait_producers): the caller writes its device input
+    on the null stream behind a long-running kernel and calls the collective at
+    once.  The ring streams are non-blocking, so without the event wait they
+    would send the old contents; with it every result matches the oracle."""
+    torch = gpu
+    world, count = 4, 300007
+    for coll in (pgamd.PG_COLL_REDUCE_SCATTER, pgamd.PG_COLL_ALL_REDUCE, pgamd.PG_COLL_ALL_GATHER):
+        xs = [oracle.fill(count, 1, 0, 9300 + r) for r in range(world)]
+        staged = [to_dev(torch, x) for x in xs]
+        S = [torch.zeros(count, dtype=torch.float64, device="cuda") for _ in xs]
+        n_out = count * world if coll == pgamd.PG_COLL_ALL_GATHER else count
+        R = [torch.zeros(n_out, dtype=torch.float64, device="cuda") for _ in xs]
+        torch.cuda.synchronize()
+        torch.cuda._sleep(200_000_000)                   # keep the null stream busy ...
+        for s_, st_ in zip(S, staged):
+            s_.copy_(st_)                                # ... and produce the inputs behind it
+        sp = (ctypes.c_void_p * world)(*[ptr(t) for t in S])
+        rp = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
+        assert lib.pgx_sim_run(world, coll, sp, rp, count, 1, 0, 1 << 16, 4096, 4, 2) == 0, pgamd.last_error()
+        if coll == pgamd.PG_COLL_REDUCE_SCATTER:
+            want = oracle.ring_reduce_scatter(xs, 1, 0, 2)
+        elif coll == pgamd.PG_COLL_ALL_REDUCE:
+            want = oracle.ring_all_reduce(xs, 1, 0, 2)
+        else:
+            want = oracle.ring_all_gather(xs, 1)
+        for r in range(world):
+            got = to_host(torch, R[r])
+            assert got[:want[r].size].tobytes() == want[r].tobytes(), (coll, r)
+
+
+@pytest.mark.parametrize("on_dev", [True, False])
+def test_config1_exact_shape_sim(gpu, lib, oracle, on_dev):
+    """BASELINE config 1 at its exact shape: 2-rank ring, DT_INT32 OP_SUM,
+    count = 1,048,576 (reference src/pg.c:264-291), through the ring executor
+    (default segments, both rings): reduce-scatter and all-reduce bit-exact
+    against the oracle's ring."""
+    world, count = 2, 1 << 20
+    xs = [oracle.fill(count, 0, 0, 0x5EEDC0DE ^ (1 << 32) ^ r) for r in range(world)]
+    want_rs = oracle.ring_reduce_scatter(xs, 0, 0, 2)
+    got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, [np.zeros(count // 2, np.int32) for _ in xs],
+              count, 0, 0, 4 << 20, 4096, 4, on_dev)
+    for r in range(world):
+        assert got[r].tobytes() == want_rs[r].tobytes()
+    want_ar = oracle.ring_all_reduce(xs, 0, 0, 2)
+    got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, np.int32) for _ in xs],
+              count, 0, 0, 4 << 20, 4096, 4, on_dev)
+    for r in range(world):
+        assert got[r].tobytes() == want_ar[r].tobytes()

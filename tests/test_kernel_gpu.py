@@ -334,3 +334,61 @@ def test_reduce_captured_in_hip_graph(gpu, lib, oracle):
             want = oracle.reduce(oracle.reduce(want, b, dt, op), c, dt, op)
         torch.cuda.synchronize()
         assert to_host(torch, A).tobytes() == want.tobytes(), (dt, op)
+
+
+def test_reduce_ranges(gpu, lib, oracle):
+    """pgk_reduce_ranges (one launch for every ring's arrived segments of an
+    executor batch): 1..8 ranges of ragged lengths at aligned and misaligned
+    offsets of one pool, in both operand orders (out = a op b with out = a, or
+    out = b -- the in-place last round's arrival-first order), each range
+    bit-exact against the oracle's reduce of the same operands."""
+    import ctypes
+    torch = gpu
+    rng = np.random.default_rng(7)
+    VP, SZ = ctypes.c_void_p, ctypes.c_size_t
+    for trial in range(40):
+        dt, op = int(rng.integers(2)), int(rng.integers(2))
+        es = 4 if dt == 0 else 8
+        k = int(rng.integers(1, 9))
+        lens = [int(rng.choice([0, 1, 3, 5, 64, 1000, 4099, 65536 + 7, 1 << 20])) for _ in range(k)]
+        shift = int(rng.integers(0, 4)) if trial % 3 == 0 else 0      # misaligned: one range off by elements
+        size = sum(2 * (n + 8) for n in lens) + 16
+        a_np = oracle.fill(size, dt, op, 100 + trial)
+        b_np = oracle.fill(size, dt, op, 200 + trial)
+        A, B = to_dev(torch, a_np), to_dev(torch, b_np)
+        outs, as_, bs_, ns = (VP * k)(), (VP * k)(), (VP * k)(), (SZ * k)()
+        want_a, want_b = a_np.copy(), b_np.copy()
+        off = 0
+        for j, n in enumerate(lens):
+            o = off + (shift if j == k - 1 else 0)
+            rev = (j + trial) % 2 == 1
+            pa, pb = ptr(A) + o * es, ptr(B) + o * es
+            if rev:       # out = b = a op b
+                outs[j], as_[j], bs_[j] = pb, pa, pb
+                want_b[o:o + n] = oracle.reduce(a_np[o:o + n], b_np[o:o + n], dt, op)
+            else:         # out = a = a op b
+                outs[j], as_[j], bs_[j] = pa, pa, pb
+                want_a[o:o + n] = oracle.reduce(a_np[o:o + n], b_np[o:o + n], dt, op)
+            ns[j] = n
+            off += n + 8
+        assert lib.pgk_reduce_ranges(outs, as_, bs_, ns, k, dt, op, stream(torch), None, None) == 0, \
+            pgamd.last_error()
+        assert to_host(torch, A).tobytes() == want_a.tobytes(), (trial, lens, shift)
+        assert to_host(torch, B).tobytes() == want_b.tobytes(), (trial, lens, shift)
+    # argument checks and stamps
+    assert lib.pgk_reduce_ranges(None, None, None, None, 0, 1, 0, stream(torch), None, None) == 0
+    nine = (VP * 9)()
+    assert lib.pgk_reduce_ranges(nine, nine, nine, (SZ * 9)(), 9, 1, 0, stream(torch), None, None) == -1
+    x = torch.ones(1 << 20, dtype=torch.float64, device="cuda")
+    ev0, ev1 = VP(), VP()
+    pgamd.check(lib.pgk_event_create(ctypes.byref(ev0)), "event")
+    pgamd.check(lib.pgk_event_create(ctypes.byref(ev1)), "event")
+    p2 = (VP * 2)(ptr(x), ptr(x) + (1 << 22))
+    assert lib.pgk_reduce_ranges(p2, p2, p2, (SZ * 2)(1 << 18, 1 << 18), 2, 1, 0, stream(torch), ev0, ev1) == 0
+    torch.cuda.synchronize()
+    ms = ctypes.c_float()
+    pgamd.check(lib.pgk_event_elapsed_ms(ev0, ev1, ctypes.byref(ms)), "elapsed")
+    assert ms.value > 0
+    assert float(x[:1 << 18].sum()) == 2.0 * (1 << 18) and float(x[1 << 18:1 << 19].sum()) == 1 << 18
+    lib.pgk_event_destroy(ev0)
+    lib.pgk_event_destroy(ev1)

@@ -164,3 +164,19 @@ def test_plan_all_gather_matches_oracle(oracle, world, rings):
         got = ring_all_gather(xs, dt, rings)
         for r in range(world):
             assert got[r].tobytes() == want[r].tobytes()
+
+
+@pytest.mark.parametrize("rings", [1, 2, 4])
+def test_in_place_last_round_keeps_arrival_first(rings):
+    """Only the in-place all-reduce's last round folds into SRC's own block;
+    it is marked red_rev so the executor computes arrival op own like every
+    other round (the left operand decides the payload of NaN op NaN)."""
+    world = 5
+    for alias in (0, 1):
+        st = pgamd.plan_reduce_scatter(2, world, 10007, 1, 1 << 12, 0, 3, alias, rings)
+        for s in st:
+            last = s["round"] == world - 2
+            assert s["red_rev"] == (1 if alias and last and s["red_elems"] else 0), s
+            if s["red_rev"]:
+                assert s["red_dst_buf"] == pgamd.PG_BUF_OUT and s["red_src_buf"] in (pgamd.PG_BUF_STAGE0,
+                                                                                      pgamd.PG_BUF_STAGE1)

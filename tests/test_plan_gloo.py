@@ -76,7 +76,7 @@ def _worker(rank, world, port, q):
                         n = s["red_elems"] * es
                         d = bufs[s["red_dst_buf"]][s["red_dst_off"]:s["red_dst_off"] + n].view(NP[dt])
                         src = bufs[s["red_src_buf"]][s["red_src_off"]:s["red_src_off"] + n].view(NP[dt])
-                        np_reduce(d, src, op)
+                        np_reduce(d, src, op, s["red_rev"])
                 i = j
             got = bufs[pgamd.PG_BUF_OUT].view(NP[dt])
             if got.tobytes() != want.tobytes():

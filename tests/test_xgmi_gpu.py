@@ -21,6 +21,8 @@ CASES = [  # coll, dt, op, count, on_dev, in_place
     ("ar", 1, 0, 100003, True, False), ("ar", 0, 1, 999, False, False), ("ar", 1, 1, 4096, True, True),
     ("ar", 0, 0, 7, False, True), ("rs", 1, 0, 5000, True, False), ("ar", 1, 0, 300001, True, False),
     ("ar", 0, 1, 524288, False, True),
+    # BASELINE config 1's exact shape (int32 sum, count 1,048,576; reference src/pg.c:264-291)
+    ("rs", 0, 0, 1 << 20, True, False), ("ar", 0, 0, 1 << 20, True, False),
     # "mixed": even ranks pass device buffers, odd ranks host buffers -> every
     # rank must agree to fall back from zero-copy to the slot copy
     ("rs", 1, 0, 77777, "mixed", False), ("ar", 0, 0, 300000, "mixed", False), ("ag", 1, 0, 999, "mixed", False),
