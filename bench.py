@@ -607,6 +607,41 @@ def _phases(h, rank, world):
     return out
 
 
+def _small_calls(lib, h, rank, world, reps=50):
+    """Config 5's eager-size calls on their own: 4 KiB per rank (512 doubles,
+    product), reduce-scatter and all-reduce on device buffers, `reps` calls
+    each; per-call wall time (median / p90 over calls, slowest rank) and the
+    phase breakdown of the last call (pg_get_stats: wall, device part, and
+    the xgmi transport's producer wait / barrier / kernel phases)."""
+    count = 512
+    x = _pattern(count, rank, world, pgamd.DT_DOUBLE, pgamd.OP_PROD)
+    off, ln = pgamd.block_range(count, world, rank)
+    out = {}
+    for name in ("reduce_scatter", "all_reduce"):
+        y = torch.empty(count if name == "all_reduce" else max(ln, 1), dtype=torch.float64, device="cuda")
+        fn = lib.pg_all_reduce if name == "all_reduce" else lib.pg_reduce_scatter
+        for _ in range(5):
+            pgamd.check(fn(x.data_ptr(), y.data_ptr(), count, pgamd.DT_DOUBLE, pgamd.OP_PROD, h), name)
+        barrier(world)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            pgamd.check(fn(x.data_ptr(), y.data_ptr(), count, pgamd.DT_DOUBLE, pgamd.OP_PROD, h), name)
+            ts.append((time.perf_counter() - t0) * 1e6)
+        barrier(world)
+        want = _expected_block(count, 0 if name == "all_reduce" else off, count if name == "all_reduce" else ln,
+                               world, pgamd.DT_DOUBLE, pgamd.OP_PROD)
+        ok = bool(torch.equal(y[:want.numel()], want))
+        st = pgamd.stats(h)
+        out[name] = {"us_median": round(max_over_ranks(float(np.median(ts)), world), 1),
+                     "us_p90": round(max_over_ranks(float(np.percentile(ts, 90)), world), 1),
+                     "ok": sum_over_ranks(1.0 if ok else 0.0, world) == world,
+                     "last_call": {k: round(max_over_ranks(float(st[k]), world), 1)
+                                   for k in ("wall_us", "ring_us", "sync_us", "copy_us", "barrier_us", "kernel_us")}}
+    out["shape"] = "512 doubles (4 KiB) per rank, OP_PROD, device buffers; per-call host wall time"
+    return out
+
+
 def _in_ring_reduce(lib, h, x, out, count, dt, rank, world):
     """The reduce launches inside the ring, measured: one more reduce-scatter
     with PG_KERNEL_TIMING=1, which stamps every executor launch with its own
@@ -738,6 +773,11 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     "rings": int(os.environ.get("PG_RINGS", "2"))})
         if core_only:
             return res
+        progress(rank, f"  {transport}: 4 KiB calls")
+        try:
+            res["eager_4KiB"] = _small_calls(lib, h, rank, world)
+        except Exception as e:  # noqa: BLE001 -- a report row, never fatal for the leg
+            res["eager_4KiB"] = {"error": f"{type(e).__name__}: {e}"}
         if transport == "xgmi":          # (one-GPU rehearsal: every "link" is the same device)
             progress(rank, f"  {transport}: link probe")
             res["link_probe"] = _link_probe(lib, h, rank, world)
@@ -768,32 +808,45 @@ def ring_leg(lib, args, rank, world, transport, sink):
                                                 world) == world
         del xh, oh
         rounds = world - 1
-        if world == 4:                                    # config 3: PG_CHUNK_BYTES sweep
+        # the segment and inflight knobs only exist on the point-to-point ring
+        # (the xgmi transport reads whole blocks); each sweep marks the library
+        # default and names the fastest row -- DESIGN.md §10 states the rule
+        # that turns these rows into the next defaults
+        if world == 4 and transport == "rccl":            # config 3: PG_CHUNK_BYTES sweep
             progress(rank, f"  {transport}: chunk sweep")
             rows = []
+            default_cb = int(hd.chunk_bytes)
             for cb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20):
                 hd.chunk_bytes = cb
                 t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
                 rows.append([payload, rounds, int(hd.inflight), round(t * 1e6, 1), round(payload / t / 1e9, 2),
-                             cb])
-            hd.chunk_bytes = 4 << 20
-            res["chunk_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes"],
-                                  "rows": rows}
-        if world == 8:                                    # config 4: PG_INFLIGHT sweep
+                             cb, int(cb == default_cb)])
+            hd.chunk_bytes = default_cb
+            best = max(rows, key=lambda r: r[4])
+            res["chunk_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes",
+                                              "is_default"], "rows": rows,
+                                  "default_chunk_bytes": default_cb, "fastest_chunk_bytes": best[5],
+                                  "fastest_over_default": round(best[4] / next(r[4] for r in rows if r[6]), 3)}
+        if world == 8 and transport == "rccl":            # config 4: PG_INFLIGHT sweep
             progress(rank, f"  {transport}: inflight sweep")
             rows = []
+            default_inf = int(hd.inflight)
             for inf in (1, 2, 4, 8, 16):
                 hd.inflight = inf
                 t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
-                rows.append([payload, rounds, inf, round(t * 1e6, 1), round(payload / t / 1e9, 2)])
-            hd.inflight = 4
-            res["inflight_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s"], "rows": rows}
+                rows.append([payload, rounds, inf, round(t * 1e6, 1), round(payload / t / 1e9, 2), int(inf == default_inf)])
+            hd.inflight = default_inf
+            best = max(rows, key=lambda r: r[4])
+            res["inflight_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "is_default"],
+                                     "rows": rows, "default_inflight": default_inf, "fastest_inflight": best[2],
+                                     "fastest_over_default": round(best[4] / next(r[4] for r in rows if r[5]), 3)}
         del x, out
         torch.cuda.empty_cache()
         if world == 8:                                    # config 5: prod, eager and 2 GiB mixed
             progress(rank, f"  {transport}: config 5")
             cfg5 = []
             for dt5, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
+                big //= max(args.ring_div, 1)              # 2 GiB per rank unless rehearsing
                 small = 4096 // pgamd.ELEM_SIZE[dt5]
                 for cnt in (small, big, small):
                     xv = _pattern(cnt, rank, world, dt5, pgamd.OP_PROD)

@@ -108,42 +108,26 @@ int pg_stream_wait(hipStream_t s) {
   return 0;
 }
 
-/* Same bounded spin for an event. */
-static int pg_event_wait(hipEvent_t ev) {
-  static double spin_us = -1.0;
-  if (spin_us < 0) {
-    const char *e = getenv("PG_SPIN_US");
-    spin_us = (e && *e) ? atof(e) : 200.0;
-  }
-  double t0 = spin_us > 0 ? now_us() : 0;
-  while (spin_us > 0) {
-    hipError_t e = hipEventQuery(ev);
-    if (e == hipSuccess) return 0;
-    if (e != hipErrorNotReady) {
-      pg_set_error("event wait: %s", hipGetErrorString(e));
-      return -1;
-    }
-    if (now_us() - t0 > spin_us) break;
-    __builtin_ia32_pause();
-  }
-  PG_CHECK_HIP(hipEventSynchronize(ev));
-  return 0;
-}
-
 /* Device buffers: the caller's producers are the work it enqueued on the null
- * stream before the call -- and, through the null stream's implicit
- * synchronisation, on every blocking stream ("Device
- * buffers").  The collective must not read its buffers before that work ends.
- * The ring's streams wait for it on the device (host_wait = 0): nothing blocks
- * the host, and the first transfer is queued behind the producer.  A transport
- * whose peers read this rank's buffers once it reaches a host barrier (xgmi)
- * waits on the host instead (host_wait = 1).  Either way it is narrower than a
- * hipDeviceSynchronize(): non-blocking streams of the process that the caller
- * did not order before the call (another thread's work, RCCL's) are not
- * waited for (tests/test_api_gpu.py::test_device_input_behind_slow_producer). */
+ * stream before the call ("Device buffers"; work on other
+ * streams the caller orders before the call itself).  The collective must not
+ * read its buffers before that work ends.
+ * An idle null stream (the usual case: the caller synchronised, or produced
+ * the input by a blocking copy) is a host-side query and costs no GPU round
+ * trip.  Otherwise the ring's streams wait for it on the device (host_wait =
+ * 0): nothing blocks the host, and the first transfer is queued behind the
+ * producer.  A transport whose peers read this rank's buffers once it reaches
+ * a host barrier (xgmi) waits on the host instead (host_wait = 1).  Either way
+ * it is narrower than a hipDeviceSynchronize(): non-blocking streams of the
+ * process that the caller did not order before the call (another thread's
+ * work, RCCL's) are not waited for
+ * (tests/test_api_gpu.py::test_device_input_behind_slow_producer). */
 int pg_wait_producers(struct pg_impl *im, int host_wait) {
+  hipError_t q = hipStreamQuery(NULL);
+  if (q == hipSuccess) return 0;
+  if (q != hipErrorNotReady) { pg_set_error("null stream query: %s", hipGetErrorString(q)); return -1; }
+  if (host_wait) return pg_stream_wait(NULL);
   PG_CHECK_HIP(hipEventRecord(im->entry_ev, NULL));
-  if (host_wait) return pg_event_wait(im->entry_ev);
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->entry_ev, 0));
   PG_CHECK_HIP(hipStreamWaitEvent(im->red, im->entry_ev, 0));
   return 0;

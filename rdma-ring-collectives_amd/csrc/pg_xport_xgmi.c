@@ -53,6 +53,12 @@ struct xg_import {
   unsigned long stamp;
 };
 #define XG_GRANULE (64ull << 20)
+/* A cached mapping of a peer's input keeps that allocation's HBM alive in the
+ * peer even after it frees it.  Mappings of allocations at least this large
+ * are kept only while they are the peer's current input: the first call with
+ * another input closes them (tests/test_xgmi_gpu.py::
+ * test_xgmi_freed_large_input_is_released).  Small ones stay in the LRU. */
+#define XG_KEEP_MAX (256ull << 20)
 
 struct xg_hist {
   uint64_t base, size;
@@ -87,7 +93,7 @@ static void drop_imports(struct pg *pg, struct xgmi_ctx *x);
 
 /* ROCm 7.2: hipIpcOpenMemHandle never returns for an allocation whose size has
  * bit 31 set (2 GiB, 2 GiB + 2 MiB, 3 GiB, 6 GiB stall; 2 GiB - 2 MiB, 4, 5,
- * 8, 12 GiB open in < 1 ms; measured on MI355X, tools/ipc_probe3.py).  So no
+ * 8, 12 GiB open in < 1 ms; measured on MI355X, tools/ipc_probe.py --mode sizes).  So no
  * allocation of that size is ever exported: our own slot memory is padded to
  * the next multiple of 4 GiB, and a caller's input living in such an
  * allocation takes the slot copy instead of zero-copy. */
@@ -320,7 +326,7 @@ static struct xg_desc *descs(struct xgmi_ctx *x) {
 }
 
 /* An IPC handle names (exporter pid, address, size), not the allocation
- * (tools/ipc_probe4.py: a new allocation at a freed one's address exports
+ * (tools/ipc_probe.py --mode reuse: a new allocation at a freed one's address exports
  * byte-identical handle bytes), and what hipIpcOpenMemHandle does in an
  * importer that opened that range before is not something this transport can
  * control: it may hand back a mapping of the freed allocation (stale data,
@@ -431,6 +437,18 @@ static const char *import_input(struct xgmi_ctx *x, int q, const struct xg_desc 
   return (const char *)p + d->off;
 }
 
+/* Close this peer's cached mappings of large allocations other than `bid`
+ * (not read by the current call). */
+static void release_stale_imports(struct xgmi_ctx *x, int q, unsigned long long bid) {
+  struct xg_import *e = &x->imp[q * XG_IMPORTS];
+  for (int i = 0; i < XG_IMPORTS; ++i)
+    if (e[i].base && e[i].bid != bid && e[i].peer_size >= XG_KEEP_MAX) {
+      hipIpcCloseMemHandle(e[i].base);
+      e[i].base = NULL;
+      e[i].stamp = 0;
+    }
+}
+
 static void drop_imports(struct pg *pg, struct xgmi_ctx *x) {
   if (!x->imp) return;
   for (int i = 0; i < pg->world_size * XG_IMPORTS; ++i)
@@ -489,12 +507,16 @@ static int share_inputs(struct pg *pg, const void *in, size_t bytes, int in_dev,
                  (const void *)by_rank[q], (unsigned long long)all[q].bid, (unsigned long long)all[q].base,
                  (unsigned long long)all[q].size, (unsigned long long)all[q].off);
         if (!by_rank[q]) *fail = 2;           /* soft: every rank redoes the call with the slot copy */
+        if (q != r) release_stale_imports(x, q, all[q].bid);
       }
       *zero_copy = 1;
       im->stats.zero_copy = !*fail;
       return 0;
     }
-    /* somebody's input cannot be shared in place: everybody copies */
+    /* somebody's input cannot be shared in place: everybody copies, and no
+     * mapping of a peer's input is read by this call */
+    for (int q = 0; q < W; ++q)
+      if (q != r) release_stale_imports(x, q, 0);
   }
   /* every rank reaches this point in this call (the choice above is collective) */
   if (bytes && ensure(pg, XG_REG_X, bytes)) return -1;

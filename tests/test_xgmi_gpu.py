@@ -243,7 +243,7 @@ def test_xgmi_slot_growth(gpu, world):
 
 def _bit31_worker(rank, world, port, q):
     """Allocations whose size has bit 31 set stall hipIpcOpenMemHandle on
-    ROCm 7.2 (tools/ipc_probe3.py).  600 MiB calls need 1 GiB slots, i.e. a
+    ROCm 7.2 (tools/ipc_probe.py --mode sizes).  600 MiB calls need 1 GiB slots, i.e. a
     2 GiB two-slot region that the transport must pad: (a) a fresh input is
     read in place and the all-reduce grows the result region; (b) an input
     that lives in a 2 GiB allocation cannot be shared in place, so every rank
@@ -309,6 +309,85 @@ def test_xgmi_ipc_bit31_sizes(gpu):
         assert not fails, (rank, fails)
 
 
+def _release_worker(rank, world, port, q):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="60000")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    res = {}
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        assert lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) == 0
+        small = torch.ones(1 << 16, dtype=torch.float64, device="cuda")
+        sout = torch.empty(1 << 16, dtype=torch.float64, device="cuda")
+
+        def sync_all():          # a collective: every rank has passed the previous call
+            assert lib.pg_all_reduce(small.data_ptr(), sout.data_ptr(), 1 << 16, 1, 0, h) == 0, pgamd.last_error()
+
+        sync_all()
+        torch.cuda.synchronize()
+        res["free0"] = torch.cuda.mem_get_info()[0]
+        sync_all()
+        count = 1 << 29                                   # 4 GiB of doubles, read in place by the peers
+        x = torch.full((count,), float(rank + 1), dtype=torch.float64, device="cuda")
+        off, ln = pgamd.block_range(count, world, rank)
+        out = torch.empty(ln, dtype=torch.float64, device="cuda")
+        assert lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, 1, 0, h) == 0, pgamd.last_error()
+        res["zero_copy"] = pgamd.stats(h)["zero_copy"]
+        res["ok"] = bool((out == world * (world + 1) / 2).all())
+        del x, out
+        torch.cuda.empty_cache()                          # the caller frees its large input
+        for kind in ("in place", "slot copy"):            # the next calls read other inputs
+            y = torch.full((1 << 20,), 2.0, dtype=torch.float64, device="cuda")
+            z = y if kind == "slot copy" else torch.empty(1 << 20, dtype=torch.float64, device="cuda")
+            assert lib.pg_all_reduce(y.data_ptr(), z.data_ptr(), 1 << 20, 1, 0, h) == 0, pgamd.last_error()
+            res["ok"] &= bool((z == 2.0 * world).all())
+            del y, z
+        sync_all()
+        torch.cuda.synchronize()
+        res["free1"] = torch.cuda.mem_get_info()[0]
+        sync_all()
+        lib.pg_close(h)
+    except Exception as e:
+        res["exception"] = repr(e)
+    q.put((rank, res))
+
+
+def test_xgmi_freed_large_input_is_released(gpu):
+    """A peer's mapping of a caller's 4 GiB input must not keep that HBM alive
+    once the caller has freed it and moved on: the next call (read in place or
+    slot copy) closes large mappings it does not read.  Both ranks share the
+    one GPU, so device free memory after the sequence must be back to where it
+    was before the 4 GiB inputs (within 1 GiB of small allocations)."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_release_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=240))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, res in results:
+        assert "exception" not in res, res
+        assert res["ok"] and res["zero_copy"] == 1, res
+        assert res["free1"] > res["free0"] - (1 << 30), (rank, res["free0"] >> 20, res["free1"] >> 20)
+
+
 def _probe_worker(rank, world, port, q):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
                       PG_BARRIER_TIMEOUT_MS="60000")
@@ -363,7 +442,7 @@ def test_xgmi_link_probe(gpu, world):
 def _realloc_worker(rank, world, port, q):
     """A rank frees its input allocation and makes a new one, which lands at the
     same address (hipMalloc reuses it for equal sizes); the IPC handle of the
-    new allocation is byte-identical to the old one's (tools/ipc_probe4.py), so
+    new allocation is byte-identical to the old one's (tools/ipc_probe.py --mode reuse), so
     a peer that kept its mapping of the old allocation would be handed that
     stale mapping back by hipIpcOpenMemHandle and fold freed data."""
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
