@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Per-call latency/throughput of pg_all_reduce / pg_reduce_scatter over the
-xgmi transport with W real processes sharing this box's GPU(s) (device and
-host buffers), across message sizes from eager (4 KiB) to 256 MiB.
+xgmi transport or the RCCL ring with W real processes sharing this box's GPU(s)
+(device and host buffers), across message sizes from eager (4 KiB) to 256 MiB.
 
-    python tools/latency.py [--world 2] [--out gpurun_out/latency.csv]
+    python tools/latency.py [--world 2] [--transport xgmi|rccl] [--out gpurun_out/latency.csv]
+
+With --transport rccl on one GPU every rank gets its own NCCL_HOSTID, so RCCL
+carries the hops over its socket transport (tests/test_rccl_gpu.py): the
+small-call figures show our fixed cost plus a loopback socket round trip.
 
 Rows: size, rounds, inflight, time_us, GB/s (reference README.md:85 schema)
 plus collective / memory kind.  On a 1-GPU box all ranks share one device, so
@@ -19,15 +23,17 @@ import time
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
-def worker(rank, world, port, q, sizes):
+def worker(rank, world, port, q, sizes, transport):
     try:
-        _worker(rank, world, port, q, sizes)
+        _worker(rank, world, port, q, sizes, transport)
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, [("error", repr(e))]))
 
 
-def _worker(rank, world, port, q, sizes):
-    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port))
+def _worker(rank, world, port, q, sizes, transport):
+    os.environ.update(PG_TRANSPORT=transport, PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port))
+    if transport == "rccl":
+        os.environ.update(NCCL_HOSTID=f"pg-latency-{port}-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     import ctypes
 
@@ -62,8 +68,8 @@ def _worker(rank, world, port, q, sizes):
                         ts.append(time.perf_counter() - t0)
                 med = statistics.median(ts)
                 st = pgamd.stats(h)
-                phases = "sync %.0f copy %.0f barrier %.0f kernel %.0f wall %.0f" % (
-                    st["sync_us"], st["copy_us"], st["barrier_us"], st["kernel_us"], st["wall_us"])
+                phases = "sync %.0f copy %.0f barrier %.0f kernel %.0f device %.0f wall %.0f" % (
+                    st["sync_us"], st["copy_us"], st["barrier_us"], st["kernel_us"], st["ring_us"], st["wall_us"])
                 rows.append((nbytes, world - 1, 0, round(med * 1e6, 2), round(nbytes / med / 1e9, 3), coll, kind,
                              phases))
             del x, y
@@ -74,6 +80,7 @@ def _worker(rank, world, port, q, sizes):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--transport", default="xgmi", choices=("xgmi", "rccl"))
     ap.add_argument("--out", default="gpurun_out/latency.csv")
     a = ap.parse_args()
     import multiprocessing as mp
@@ -84,7 +91,7 @@ def main():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(r, a.world, port, q, sizes)) for r in range(a.world)]
+    ps = [ctx.Process(target=worker, args=(r, a.world, port, q, sizes, a.transport)) for r in range(a.world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(a.world))
@@ -93,6 +100,7 @@ def main():
     out = pathlib.Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
     with out.open("w") as f:
+        f.write(f"# transport {a.transport}, {a.world} processes on one GPU\n")
         f.write("size,rounds,inflight,time_us,GB/s,collective,memory,last_call_phases_us\n")
         for row in res[0]:
             f.write(",".join(map(str, row)) + "\n")
