@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r01_bench.json, printed by bench.py on
+"""The committed bench line (profiles/r02_bench.json, printed by bench.py on
 MI355X) keeps the driver's contract: BASELINE.json's metric, the required keys,
 a roofline object whose fraction is its own achieved/peak, and a CPU baseline
 naming its sample and core count.  The PMC traffic it carries must come from
@@ -20,7 +20,7 @@ def _line(name):
 
 
 def test_bench_line_keys_and_metric():
-    line = _line("r01_bench.json")
+    line = _line("r02_bench.json")
     base = json.loads((ROOT / "BASELINE.json").read_text())
     for k in REQUIRED:
         assert k in line, k
@@ -31,7 +31,7 @@ def test_bench_line_keys_and_metric():
 
 
 def test_roofline_is_self_consistent():
-    line = _line("r01_bench.json")
+    line = _line("r02_bench.json")
     r = line["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-4)
@@ -46,19 +46,40 @@ def test_roofline_is_self_consistent():
 
 
 def test_cpu_baseline_names_its_sample():
-    cpu = _line("r01_bench.json")["cpu_baseline"]
+    cpu = _line("r02_bench.json")["cpu_baseline"]
     assert cpu["kind"] in ("reference", "port") and cpu["cores"] >= 1 and cpu["value"] > 0
     assert cpu["sample"] and cpu["unit"]
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rehearsal_lines_checked_out(world):
-    line = _line(f"r01_bench_n{world}_onegpu_rehearsal.json")
-    assert line["n_gpus"] == world and line["metric"] == _line("r01_bench.json")["metric"]
+    line = _line(f"r02_bench_n{world}_onegpu_rehearsal.json")
+    assert line["n_gpus"] == world and line["metric"] == _line("r02_bench.json")["metric"]
     ring = line["ring"]
     legs = [v for v in ring.values() if isinstance(v, dict)]
     assert legs and all(v.get("ok") is True for v in legs)
     assert all(v.get("host_buffers_ok", True) is True for v in legs)
+    # round 2: every transport ran, the RCCL ring included, and nothing was redone
+    assert {"xgmi", "rccl"} <= set(ring)
     for v in legs:
         for row in v.get("config5_prod_mixed", []):
             assert row["ok"] is True
+        phases = v.get("last_call_phases", {})
+        assert phases.get("redone") is False and phases.get("calls_redone_total") == 0
+        small = v.get("eager_4KiB")
+        if small:
+            assert small["reduce_scatter"]["ok"] and small["all_reduce"]["ok"]
+        nat = v.get("rccl_native")
+        if isinstance(nat, dict):
+            assert nat["i32_sum_bit_exact"] and nat["f64_sum_within_tol"]
+
+
+def test_batch_launch_at_defaults_above_70_percent():
+    """The executor's reduce launch at the library defaults (4 MiB x 4
+    inflight x 2 rings, one pgk_reduce_ranges launch) keeps >= 70% of the HBM
+    peak, and the size table starts at the in-ring sizes."""
+    ks = _line("r02_bench.json")["kernel_sizes"]
+    assert {r[2] for r in ks["rows"]} >= {4 << 20, 16 << 20, 32 << 20, 64 << 20}
+    first = ks["ring_batches"]["rows"][0]
+    assert first[:3] == [4 << 20, 4, 2]
+    assert first[5] >= 0.70 and first[7] >= 0.70
