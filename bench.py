@@ -655,7 +655,7 @@ def _in_ring_reduce(lib, h, x, out, count, dt, rank, world):
         os.environ.pop("PG_KERNEL_TIMING", None)
     st = pgamd.stats(h)
     us = float(st["red_kernel_us"])
-    moved = 3 * int(st["reduce_elems"]) * pgamd.ELEM_SIZE[dt]
+    moved = int(st["red_kernel_bytes"])       # 3*n*es per ring reduce, (W+1)*n*es per direct fold
     gbs = moved / us / 1e3 if us > 0 else 0.0
     per = gather_over_ranks(gbs, rank, world)
     launches = int(st["reduce_launches"])
@@ -664,17 +664,20 @@ def _in_ring_reduce(lib, h, x, out, count, dt, rank, world):
             "gbs_per_rank": {"min": round(min(per), 1), "median": round(float(np.median(per)), 1),
                              "max": round(max(per), 1)},
             "frac_min": round(min(per) / HBM_PEAK_GBS, 4),
-            "timing": "PG_KERNEL_TIMING=1: each pgk_reduce_ranges launch kernel-stamped; 3 x reduced bytes / "
-                      "summed kernel time, one untimed reduce-scatter"}
+            "timing": "PG_KERNEL_TIMING=1: each reduce launch kernel-stamped (pgk_reduce_ranges on the ring, "
+                      "pgk_reduce_multi on the direct exchange); algorithmic bytes (3*n*es per ring reduce, "
+                      "(W+1)*n*es per direct fold) / summed kernel time, one untimed reduce-scatter"}
 
 
-def _ring_variant(lib, rank, world, x, out, count, dt, rings, port_off):
-    """The same timed reduce-scatter with PG_RINGS=`rings` (a second handle and
-    RCCL communicator): rings = 1 shows what the counter-rotating second ring
-    buys on this node, rings = 4 what two more rings of step +3 / -3 (over
-    other xGMI links) add.  Results are checked against the default handle's."""
-    saved = {k: os.environ.get(k) for k in ("PG_RINGS", "PG_PORT")}
-    os.environ["PG_RINGS"] = str(rings)
+def _ring_variant(lib, rank, world, x, out, count, dt, env, port_off):
+    """The same timed reduce-scatter on a second handle (and RCCL communicator)
+    opened with `env` (PG_ALGO / PG_RINGS): the W-1 round ring beside the
+    default direct exchange, one clockwise ring (what the counter-rotating
+    second ring buys), four rings (what two more rings of step +3 / -3 add).
+    int32 results are checked against the default handle's."""
+    keys = ("PG_RINGS", "PG_PORT", "PG_ALGO")
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ.update(env)
     os.environ["PG_PORT"] = str(int(saved["PG_PORT"]) + port_off)   # no other leg uses it
     h1 = ctypes.c_void_p()
     try:
@@ -684,7 +687,9 @@ def _ring_variant(lib, rank, world, x, out, count, dt, rings, port_off):
         wall = _timed_rs(lib, h1, x, out, count, dt, pgamd.OP_SUM, 3, world)
         same = bool(torch.equal(out, ref)) if dt == pgamd.DT_INT32 else None
         payload = count * pgamd.ELEM_SIZE[dt]
-        res = {"rings": rings, "steps": [pgamd.ring_offset(world, rings, g) for g in range(rings)],
+        rings = int(env.get("PG_RINGS", "2"))
+        res = {"algo": env.get("PG_ALGO", "default"), "rings": rings,
+               "steps": [pgamd.ring_offset(world, rings, g) for g in range(rings)],
                "ms_per_reduce_scatter": round(wall * 1e3, 3), "algbw_gibs": round(payload / wall / GIB, 2),
                "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2)}
         if same is not None:
@@ -744,7 +749,7 @@ def ring_leg(lib, args, rank, world, transport, sink):
     try:
         hd = pgamd.head(h)
         res = {"workload": cfg, "transport": {
-            "rccl": "RCCL P2P ring over xGMI",
+            "rccl": "RCCL point-to-point over xGMI (PG_ALGO default: direct one-hop exchange on one node)",
             "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order",
             "xgmi_push": "each block written to its owner over xGMI (HIP IPC), folded locally in ring order"}[transport]}
         if os.environ.get("PG_BENCH_ONE_GPU") == "1":
@@ -770,6 +775,7 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
                     "reduced_traffic_gibs_per_gpu": round(3 * payload * (world - 1) / world / wall / GIB, 2),
                     "chunk_bytes": int(hd.chunk_bytes), "inflight": int(hd.inflight),
+                    "algo": (os.environ.get("PG_ALGO") or "default") if transport == "rccl" else None,
                     "rings": int(os.environ.get("PG_RINGS", "2"))})
         if core_only:
             return res
@@ -782,11 +788,14 @@ def ring_leg(lib, args, rank, world, transport, sink):
             progress(rank, f"  {transport}: link probe")
             res["link_probe"] = _link_probe(lib, h, rank, world)
         if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
-            variants = [("one_ring", 1, 6)] + ([("four_rings", 4, 8)] if world >= 5 else [])
-            for key, nr, port_off in variants:
-                progress(rank, f"  {transport}: {nr}-ring comparison")
+            variants = [("ring_algo", {"PG_ALGO": "ring", "PG_RINGS": "2"}, 4),
+                        ("one_ring", {"PG_ALGO": "ring", "PG_RINGS": "1"}, 6)]
+            if world >= 5:
+                variants.append(("four_rings", {"PG_ALGO": "ring", "PG_RINGS": "4"}, 8))
+            for key, env, port_off in variants:
+                progress(rank, f"  {transport}: {key} comparison")
                 try:
-                    res[key] = _ring_variant(lib, rank, world, x, out, count, dt, nr, port_off)
+                    res[key] = _ring_variant(lib, rank, world, x, out, count, dt, env, port_off)
                 except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
                     res[key] = {"error": f"{type(e).__name__}: {e}"}
         progress(rank, f"  {transport}: RCCL-native cross-check")

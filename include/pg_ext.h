@@ -122,7 +122,14 @@ PG_API int pg_connect_local(int rank, int world, int transport, void **out_handl
 /* Run one collective over `world` virtual ranks in this process (transport
  * THREADS): rank r uses sendbufs[r] / recvbufs[r] (HIP device or host
  * memory).  coll: 0 reduce-scatter, 1 all-gather, 2 all-reduce.  rings:
- * 1 .. PG_MAX_RINGS, 0 = PG_RINGS / the default. */
+ * 1 .. PG_MAX_RINGS, 0 = PG_RINGS / the default.  The schedule is the W-1
+ * round ring unless PG_ALGO=direct.
+ *
+ * PG_ALGO (point-to-point transports: rccl, threads): "ring" = the W-1 round
+ * ring (pg_plan.c / pg_exec.c); "direct" = block q sent straight to rank q
+ * over its own link, block r folded from all W copies in ring order
+ * (pg_direct.c), same bits.  Unset: direct when every server-list entry names
+ * the same host and W <= 16, else ring. */
 #define PG_COLL_REDUCE_SCATTER 0
 #define PG_COLL_ALL_GATHER     1
 #define PG_COLL_ALL_REDUCE     2
@@ -156,8 +163,10 @@ struct pg_stats {
   int32_t zero_copy;     /* xgmi: 1 = peers read this call's inputs in place */
   int32_t retried;       /* xgmi: 1 = redone with the slot copy (a peer input failed to map) */
   int64_t calls_redone;  /* xgmi: calls redone that way on this handle so far (cumulative) */
-  double red_kernel_us;  /* ring: summed kernel time of the reduce launches, when
-                            PG_KERNEL_TIMING=1 stamps each launch (else 0)   */
+  double red_kernel_us;  /* P2P transports: summed kernel time of the reduce launches,
+                            when PG_KERNEL_TIMING=1 stamps each launch (else 0) */
+  int64_t red_kernel_bytes; /* algorithmic HBM bytes of those launches: 3*n*es per
+                            ring reduce, (W+1)*n*es per direct fold            */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

@@ -63,6 +63,10 @@ PG_API int pgk_reduce_ranges(void *const *outs, const void *const *as, const voi
  * bit-identical to the W-1 ring steps of reduce_inplace it fuses. */
 PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                      void *stream);
+/* The same launch with the kernel's own begin/end timestamps recorded into two
+ * HIP events (as pgk_reduce_timed; NULL events = untimed). */
+PG_API int pgk_reduce_multi_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
+                                  void *stream, void *start_event, void *stop_event);
 
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]

@@ -258,6 +258,16 @@ int pg_impl_create(struct pg *pg) {
   PG_CHECK_HIP(hipEventCreate(&im->t1));
   const char *e = getenv("PG_EAGER_ONESHOT");
   im->eager_oneshot = !(e && *e && atoi(e) == 0);
+  /* PG_ALGO: ring | direct; unset: direct when every rank is on this node
+   * (connect_process_group), the ring for in-process virtual ranks */
+  im->algo = PG_ALGO_RING;
+  e = getenv("PG_ALGO");
+  if (e && *e) {
+    if (strcmp(e, "direct") == 0) im->algo = PG_ALGO_DIRECT;
+    else if (strcmp(e, "ring") != 0) { pg_set_error("PG_ALGO=%s: expected ring or direct", e); return -1; }
+  } else if (pg->hosts && pg_default_transport(pg) == PG_TRANSPORT_XGMI) {
+    im->algo = PG_ALGO_DIRECT;                   /* one node, W <= 16: every peer one link away */
+  }
   im->rings = 2;
   e = getenv("PG_RINGS");
   if (e && *e) {
@@ -397,18 +407,23 @@ static void stats_begin(struct pg_impl *im) {
   im->kt_used = 0;
 }
 
-static int sync_ring(struct pg_impl *im, int timed) {
-  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
-  if (timed) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
-  }
+/* After the streams drained: sum the stamped launches of this call. */
+void pg_kt_collect(struct pg_impl *im) {
   for (int u = 0; u < im->kt_used; ++u) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, im->kt_ev[2 * u], im->kt_ev[2 * u + 1]) == hipSuccess)
       im->stats.red_kernel_us += (double)ms * 1e3;
   }
   im->kt_used = 0;
+}
+
+static int sync_ring(struct pg_impl *im, int timed) {
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
+  if (timed) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
+  }
+  pg_kt_collect(im);
   return 0;
 }
 
@@ -652,6 +667,8 @@ int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype
     rc = pg_xgmi_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else if (pg_eager_applies(pg, count, datatype))
     rc = pg_eager_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_direct_applies(pg, count))
+    rc = pg_direct_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;
@@ -744,6 +761,8 @@ int pg_all_gather(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, vo
     rc = pg_xgmi_all_gather(pg, sendbuf, recvbuf, count, datatype);
   else if (pg_eager_applies(pg, count, datatype))
     rc = pg_eager_all_gather(pg, sendbuf, recvbuf, count, datatype);
+  else if (pg_direct_applies(pg, count))
+    rc = pg_direct_all_gather(pg, sendbuf, recvbuf, count, datatype);
   else
     rc = ring_all_gather(pg, sendbuf, recvbuf, count, datatype);
   im->stats.wall_us = now_us() - t;
@@ -840,6 +859,8 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
     rc = pg_xgmi_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   else if (pg_eager_applies(pg, count, datatype))
     rc = pg_eager_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_direct_applies(pg, count))
+    rc = pg_direct_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;

@@ -1,0 +1,270 @@
+/*
+ * pg_direct.c -- PG_ALGO=direct: the point-to-point collectives as one-hop
+ * exchanges over every link at once, for a fully connected node.
+ *
+ * The reference's ring (README.md:68-71, mocked at src/pg.c:277-289) moves
+ * each block W-1 hops, one link direction per ring, and reduces it once per
+ * hop.  On one MI355X node every GPU has its own xGMI link to each of its 7
+ * peers, so the same reduce-scatter can send block q of this rank's input
+ * straight to rank q -- all W-1 links busy, every byte crossing one link once
+ * -- and fold the W contributions of block r in ONE multi-source launch per
+ * segment batch.  The fold keeps each ring part's order
+ *     part g of block r:  x[r+d] op x[r+2d] op ... op x[r]     (d = step of ring g)
+ * so the result is bit-identical to the ring (and to the oracle) for the same
+ * PG_RINGS, doubles included.  HBM traffic drops too: (W+1)·B·es for the fold
+ * instead of 3·(W-1)·B·es for W-1 ring reduces.
+ *
+ * Pipelining: block r is cut into the ring's parts, each part into
+ * chunk_bytes segments; one transport group per `inflight` segments carries
+ * that batch from every peer (and the matching segments of every peer's block
+ * to it), and the reduce stream folds a batch as soon as its group has landed
+ * while the next batch is on the wire.  Every block uses the segment layout of
+ * the full block (empty segments in a short last block), so every rank builds
+ * the same groups and per-peer send/receive order matches.  The received
+ * segments go to a gather area of W block-sized slots, never reused inside a
+ * call, so the comm stream never waits for a fold.
+ *
+ * All-gather and the all-reduce's gather half: one group, every rank sending
+ * its block (slot) to every peer.
+ *
+ * Default for the point-to-point transports when every rank is on one node and
+ * W <= 16 (PG_ALGO unset); PG_ALGO=ring keeps the W-1 round ring.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "pg_impl.h"
+
+#define DIRECT_MAX_WORLD 16
+
+int pg_direct_applies(const struct pg *pg, int count) {
+  const struct pg_impl *im = (const struct pg_impl *)pg->impl;
+  return im->algo == PG_ALGO_DIRECT && pg->world_size > 1 && pg->world_size <= DIRECT_MAX_WORLD && count > 0;
+}
+
+/* Segment s of the flat segment list (ring parts in order, each cut into
+ * `seg`-element pieces, counted on the FULL block of `full` elements) applied
+ * to a block of `len` elements: [*off, *off + *n) inside the block, and the
+ * ring part it belongs to.  Returns 0 past the end of the list. */
+struct seglist {
+  int rings;
+  size_t full, seg;
+  int count[PG_MAX_RINGS];      /* segments per part (full block) */
+  int total;
+};
+
+static void seglist_init(struct seglist *sl, size_t full, int rings, size_t seg) {
+  memset(sl, 0, sizeof(*sl));
+  sl->rings = rings;
+  sl->full = full;
+  sl->seg = seg ? seg : 1;
+  for (int g = 0; g < rings; ++g) {
+    size_t po, pl;
+    pg_block_part(full, rings, g, &po, &pl);
+    sl->count[g] = (int)((pl + sl->seg - 1) / sl->seg);
+    sl->total += sl->count[g];
+  }
+}
+
+static int seglist_get(const struct seglist *sl, int s, size_t len, int *part, size_t *off, size_t *n) {
+  int g = 0;
+  while (g < sl->rings && s >= sl->count[g]) s -= sl->count[g++];
+  if (g >= sl->rings) return 0;
+  size_t po, pl;
+  pg_block_part(len, sl->rings, g, &po, &pl);
+  size_t a = (size_t)s * sl->seg, b = a + sl->seg;
+  if (a > pl) a = pl;
+  if (b > pl) b = pl;
+  *part = g;
+  *off = po + a;
+  *n = b - a;
+  return 1;
+}
+
+static int direct_finish(struct pg_impl *im) {
+  PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
+  PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
+  pg_kt_collect(im);
+  return 0;
+}
+
+/* Reduce-scatter core: block `rank` of the reduction of every rank's `src`
+ * (device, count elements) into `out` (device, the block's length). */
+static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const int W = pg->world_size, r = pg->rank;
+  const size_t es = pg_elem_size(dt), full = ((size_t)count + (size_t)W - 1) / (size_t)W;
+  size_t boff, blen;
+  pg_block_range(count, W, r, &boff, &blen);
+  if (pg_ensure(&im->ebuf, &im->ebuf_cap, (size_t)W * full * es)) return -1;
+  char *gat = (char *)im->ebuf;                      /* slot q: rank q's copy of block r */
+  struct seglist sl;
+  size_t seg = pg->chunk_bytes / es;
+  seglist_init(&sl, full, im->rings, seg);
+  const int inflight = pg->inflight > 0 ? pg->inflight : 1;
+  int dsteps[PG_MAX_RINGS];
+  for (int g = 0; g < im->rings; ++g) dsteps[g] = pg_ring_offset(W, im->rings, g);
+
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  int nb = 0;
+  for (int s0 = 0; s0 < sl.total; s0 += inflight, ++nb) {
+    const int s1 = s0 + inflight < sl.total ? s0 + inflight : sl.total;
+    if (im->ops->group_start(im)) return -1;
+    for (int k = 1; k < W; ++k) {                    /* peers r+1, r+2, ...: spread over the links */
+      const int q = (r + k) % W;
+      size_t qoff, qlen;
+      pg_block_range(count, W, q, &qoff, &qlen);
+      for (int s = s0; s < s1; ++s) {
+        int part;
+        size_t o, n;
+        if (seglist_get(&sl, s, qlen, &part, &o, &n) && n) {
+          if (im->ops->send(im, src + (qoff + o) * es, n * es, q, im->comm)) return -1;
+          im->stats.bytes_sent += (int64_t)(n * es);
+        }
+        if (seglist_get(&sl, s, blen, &part, &o, &n) && n) {
+          if (im->ops->recv(im, gat + ((size_t)q * full + o) * es, n * es, q, im->comm)) return -1;
+          im->stats.bytes_recv += (int64_t)(n * es);
+        }
+      }
+    }
+    if (im->ops->group_end(im, im->comm)) return -1;
+    hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
+    PG_CHECK_HIP(hipEventRecord(rev, im->comm));
+    PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
+    /* fold the batch: one multi-source launch per run of segments of one part */
+    int s = s0;
+    while (s < s1) {
+      int part, part2;
+      size_t o, n, o2, n2;
+      seglist_get(&sl, s, blen, &part, &o, &n);
+      int e = s + 1;
+      while (e < s1 && seglist_get(&sl, e, blen, &part2, &o2, &n2) && part2 == part && o2 == o + n) {
+        n += n2;
+        ++e;
+      }
+      if (n) {
+        const void *srcs[DIRECT_MAX_WORLD];
+        for (int j = 0; j < W; ++j) {
+          const int q = ((r + (j + 1) * dsteps[part]) % W + W) % W;     /* j = W-1: q = r */
+          srcs[j] = q == r ? (const void *)(src + (boff + o) * es) : (const void *)(gat + ((size_t)q * full + o) * es);
+        }
+        void *t0 = NULL, *t1 = NULL;
+        if (im->kt_on) {
+          if (pg_kt_pair(im, &t0, &t1)) return -1;
+          im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * n * es);
+        }
+        if (pgk_reduce_multi_timed(out + o * es, srcs, W, n, dt, op, (void *)im->red, t0, t1)) {
+          pg_set_error("direct: %s", pgk_last_error());
+          return -1;
+        }
+        im->stats.reduce_launches++;
+        im->stats.reduce_elems += (int64_t)n * (W - 1);
+      }
+      s = e;
+    }
+  }
+  return 0;
+}
+
+/* One group: this rank's block to every peer, every peer's block into `full`.
+ * uniform: blocks of `count` elements (all-gather); else the reduce-scatter
+ * partition of `count` (the all-reduce's second half). */
+static int direct_gather_core(struct pg *pg, char *full, int count, int uniform, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const int W = pg->world_size, r = pg->rank;
+  const size_t es = pg_elem_size(dt);
+  size_t roff, rlen;
+  if (uniform) { roff = (size_t)r * (size_t)count; rlen = (size_t)count; }
+  else pg_block_range(count, W, r, &roff, &rlen);
+  if (im->ops->group_start(im)) return -1;
+  for (int k = 1; k < W; ++k) {
+    const int to = (r + k) % W, from = ((r - k) % W + W) % W;
+    size_t foff, flen;
+    if (uniform) { foff = (size_t)from * (size_t)count; flen = (size_t)count; }
+    else pg_block_range(count, W, from, &foff, &flen);
+    if (rlen && im->ops->send(im, full + roff * es, rlen * es, to, im->comm)) return -1;
+    if (flen && im->ops->recv(im, full + foff * es, flen * es, from, im->comm)) return -1;
+    im->stats.bytes_sent += (int64_t)(rlen * es);
+    im->stats.bytes_recv += (int64_t)(flen * es);
+  }
+  return im->ops->group_end(im, im->comm);
+}
+
+/* Device image of a (possibly host) input. */
+static int device_src(struct pg_impl *im, const void *buf, int dev, size_t bytes, const char **out) {
+  if (dev) { *out = (const char *)buf; return 0; }
+  if (pg_ensure(&im->dsrc, &im->dsrc_cap, bytes)) return -1;
+  if (pg_timed_copy(im->dsrc, buf, bytes, &im->stats.h2d_us)) return -1;
+  *out = (const char *)im->dsrc;
+  return 0;
+}
+
+int pg_direct_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const size_t es = pg_elem_size(dt), bytes = (size_t)count * es;
+  size_t boff, blen;
+  pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
+  int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
+  const char *src;
+  if (device_src(im, sendbuf, sd, bytes, &src)) return -1;
+  char *out = (char *)recvbuf;
+  int post_copy = 0;
+  if (!rd || pg_ranges_overlap(recvbuf, blen * es, src, bytes)) {
+    if (pg_ensure(&im->dout, &im->dout_cap, blen * es)) return -1;
+    out = (char *)im->dout;
+    post_copy = 1;
+  }
+  if (direct_rs_core(pg, src, out, count, dt, op) || direct_finish(im)) return -1;
+  if (post_copy && blen && pg_timed_copy(recvbuf, out, blen * es, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+int pg_direct_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const size_t slot = (size_t)count * pg_elem_size(dt), total = slot * (size_t)pg->world_size;
+  int rd = pg_is_device_ptr(recvbuf), sd = sendbuf && pg_is_device_ptr(sendbuf);
+  if ((rd || sd) && pg_wait_producers(im, 0)) return -1;
+  char *full = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, total)) return -1;
+    full = (char *)im->dout;
+  }
+  char *own = full + (size_t)pg->rank * slot;
+  const void *mine = sendbuf ? sendbuf : (const void *)((char *)recvbuf + (size_t)pg->rank * slot);
+  if ((const char *)mine != own && pg_timed_copy(own, mine, slot, sd || rd ? &im->stats.copy_us : &im->stats.h2d_us))
+    return -1;
+  PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  if (direct_gather_core(pg, full, count, 1, dt) || direct_finish(im)) return -1;
+  if (!rd && pg_timed_copy(recvbuf, full, total, &im->stats.d2h_us)) return -1;
+  return 0;
+}
+
+int pg_direct_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const size_t es = pg_elem_size(dt), bytes = (size_t)count * es;
+  size_t boff, blen;
+  pg_block_range(count, pg->world_size, pg->rank, &boff, &blen);
+  int sd = pg_is_device_ptr(sendbuf), rd = pg_is_device_ptr(recvbuf);
+  if ((sd || rd) && pg_wait_producers(im, 0)) return -1;
+  char *work = (char *)recvbuf;
+  if (!rd) {
+    if (pg_ensure(&im->dout, &im->dout_cap, bytes)) return -1;
+    work = (char *)im->dout;
+  }
+  if (sendbuf != (void *)work && pg_timed_copy(work, sendbuf, bytes, sd ? &im->stats.copy_us : &im->stats.h2d_us))
+    return -1;
+  /* block `rank` is folded in place: the fold reads this rank's own copy of the
+   * block element by element before writing it, and the sends read the other
+   * blocks only */
+  if (direct_rs_core(pg, work, work + boff * es, count, dt, op)) return -1;
+  PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));   /* the gather sends the folded block */
+  if (direct_gather_core(pg, work, count, 0, dt) || direct_finish(im)) return -1;
+  if (!rd && pg_timed_copy(recvbuf, work, bytes, &im->stats.d2h_us)) return -1;
+  return 0;
+}

@@ -76,7 +76,7 @@ struct red_batch {
 };
 
 /* Next start/stop event pair for a stamped launch (PG_KERNEL_TIMING=1). */
-static int kt_pair(struct pg_impl *im, void **t0, void **t1) {
+int pg_kt_pair(struct pg_impl *im, void **t0, void **t1) {
   if (2 * (im->kt_used + 1) > im->n_kt_ev) {
     int cap = im->n_kt_ev ? 2 * im->n_kt_ev : 64;
     hipEvent_t *ev = (hipEvent_t *)realloc(im->kt_ev, sizeof(hipEvent_t) * (size_t)cap);
@@ -101,12 +101,14 @@ static int kt_pair(struct pg_impl *im, void **t0, void **t1) {
 static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op) {
   if (!rb->k) return 0;
   void *t0 = NULL, *t1 = NULL;
-  if (im->kt_on && kt_pair(im, &t0, &t1)) return -1;
+  if (im->kt_on && pg_kt_pair(im, &t0, &t1)) return -1;
   if (pgk_reduce_ranges(rb->out, rb->a, rb->b, rb->n, rb->k, dt, op, (void *)im->red, t0, t1)) {
     pg_set_error("pg_exec: %s", pgk_last_error());
     return -1;
   }
   im->stats.reduce_launches += 1;
+  if (im->kt_on)
+    for (int j = 0; j < rb->k; ++j) im->stats.red_kernel_bytes += (int64_t)(3 * rb->n[j] * pg_elem_size(dt));
   rb->k = 0;
   return 0;
 }

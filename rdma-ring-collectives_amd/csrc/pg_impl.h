@@ -74,6 +74,7 @@ struct pg_impl {
   void *ebuf;      size_t ebuf_cap;   /* eager one-shot gather area (pg_eager.c) */
   int eager_oneshot;          /* PG_EAGER_ONESHOT, default 1                  */
   int rings;                  /* PG_RINGS: 1 .. 4, default 2, pg_ext.h         */
+  int algo;                   /* PG_ALGO: PG_ALGO_RING / PG_ALGO_DIRECT (P2P transports) */
 
   struct pg_step *steps; int steps_cap;
   int *boot_fds;              /* bootstrap star (pg_boot.c), world_size slots */
@@ -96,6 +97,14 @@ int pg_ranges_overlap(const void *a, size_t na, const void *b, size_t nb);
 int pg_timed_copy(void *dst, const void *src, size_t bytes, double *acc_us);  /* any direction */
 int pg_default_transport(const struct pg *pg);            /* no PG_TRANSPORT: xgmi on one node, else rccl */
 
+/* pg_direct.c: one-hop exchanges over every link, fold in ring order (P2P transports) */
+#define PG_ALGO_RING   0
+#define PG_ALGO_DIRECT 1
+int pg_direct_applies(const struct pg *pg, int count);
+int pg_direct_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
+int pg_direct_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt);
+int pg_direct_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
+
 /* pg_eager.c: one group + one launch for messages <= eager_max (P2P transports) */
 int pg_eager_applies(const struct pg *pg, int count, int dt);
 int pg_eager_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
@@ -108,6 +117,8 @@ int pg_eager_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, 
  * stream behind round k-1's transfers -- exists: the host-staging pipeline
  * uploads/downloads blocks there while the GPU runs the ring. */
 typedef int (*pg_round_hook)(struct pg_impl *im, void *ctx, int round);
+int pg_kt_pair(struct pg_impl *im, void **t0, void **t1);   /* PG_KERNEL_TIMING: next stamp pair */
+void pg_kt_collect(struct pg_impl *im);                     /* sum them once the streams drained */
 int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
                  void *const bufs[5], int dt, int op, pg_round_hook hook, void *hook_ctx);
 

@@ -483,7 +483,7 @@ hipError_t launch_ranges_t(T* const* outs, const T* const* as, const T* const* b
 }
 
 template <typename T, int OP>
-hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s) {
+hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s, Timing tm) {
   SrcList<T> sl{};
   uintptr_t m = (uintptr_t)out & 15;
   bool congruent = (m % sizeof(T)) == 0;
@@ -502,20 +502,20 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
     dim3 grid((unsigned)g), block(kMultiVecBlock);
     switch (nsrc) {
 #define PGK_MULTI_CASE(K) \
-      case K: hipLaunchKernelGGL((k_reduce_multi_vec<T, OP, K>), grid, block, 0, s, out, sl, nsrc, \
-                                 (unsigned)head, nvec, (unsigned)tail); break;
+      case K: hipExtLaunchKernelGGL((k_reduce_multi_vec<T, OP, K>), grid, block, 0, s, tm.start, tm.stop, 0, out, sl, \
+                                    nsrc, (unsigned)head, nvec, (unsigned)tail); break;
       PGK_MULTI_CASE(1) PGK_MULTI_CASE(2) PGK_MULTI_CASE(3) PGK_MULTI_CASE(4)
       PGK_MULTI_CASE(5) PGK_MULTI_CASE(6) PGK_MULTI_CASE(7) PGK_MULTI_CASE(8)
 #undef PGK_MULTI_CASE
       default:
-        hipLaunchKernelGGL((k_reduce_multi_vec<T, OP, 0>), grid, block, 0, s, out, sl, nsrc, (unsigned)head,
-                           nvec, (unsigned)tail);
+        hipExtLaunchKernelGGL((k_reduce_multi_vec<T, OP, 0>), grid, block, 0, s, tm.start, tm.stop, 0, out, sl, nsrc,
+                              (unsigned)head, nvec, (unsigned)tail);
     }
   } else {
     size_t g = (n + kMultiBlock - 1) / kMultiBlock;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP>), dim3((unsigned)g), dim3(kMultiBlock), 0, s, out, sl,
-                       nsrc, n);
+    hipExtLaunchKernelGGL((k_reduce_multi_scalar<T, OP>), dim3((unsigned)g), dim3(kMultiBlock), 0, s, tm.start,
+                          tm.stop, 0, out, sl, nsrc, n);
   }
   return hipGetLastError();
 }
@@ -524,7 +524,8 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
 
 extern "C" {
 
-int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream) {
+int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
+                           void* start_event, void* stop_event) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
@@ -533,20 +534,25 @@ int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int
   for (int j = 0; j < nsrc; ++j)
     if (!srcs[j]) { set_err("pgk: NULL source %d", j); return -1; }
   hipStream_t s = (hipStream_t)stream;
+  Timing tm{(hipEvent_t)start_event, (hipEvent_t)stop_event};
   hipError_t e;
   if (dt == PGK_DT_INT32) {
     const uint32_t* const* x = (const uint32_t* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s)
-                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s);
+    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s, tm)
+                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s, tm);
   } else {
     const double* const* x = (const double* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s)
-                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s);
+    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s, tm)
+                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s, tm);
   }
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
   return 0;
 }
 
+
+int pgk_reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream) {
+  return pgk_reduce_multi_timed(out, srcs, nsrc, n, dt, op, stream, nullptr, nullptr);
+}
 
 // Step of ring `part` among `rings` over `world` ranks: +1, -1, then +3, -3,
 // ... kept when coprime with world and new mod world, repeating when they run

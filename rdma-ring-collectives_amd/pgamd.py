@@ -57,7 +57,7 @@ class PgStats(ctypes.Structure):
         ("bytes_sent", ctypes.c_int64), ("bytes_recv", ctypes.c_int64),
         ("sync_us", ctypes.c_double), ("copy_us", ctypes.c_double), ("barrier_us", ctypes.c_double),
         ("kernel_us", ctypes.c_double), ("zero_copy", ctypes.c_int32), ("retried", ctypes.c_int32),
-        ("calls_redone", ctypes.c_int64), ("red_kernel_us", ctypes.c_double),
+        ("calls_redone", ctypes.c_int64), ("red_kernel_us", ctypes.c_double), ("red_kernel_bytes", ctypes.c_int64),
     ]
 
 
@@ -100,6 +100,7 @@ _SIGS = {
     "pgk_reduce_out": (_I, [_VP, _CVP, _CVP, _SZ, _I, _I, _VP]),
     "pgk_reduce_ranges": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ),
                                _I, _I, _I, _VP, _VP, _VP]),
+    "pgk_reduce_multi_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),

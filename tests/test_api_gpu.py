@@ -462,3 +462,78 @@ def test_config1_exact_shape_sim(gpu, lib, oracle, on_dev):
               count, 0, 0, 4 << 20, 4096, 4, on_dev)
     for r in range(world):
         assert got[r].tobytes() == want_ar[r].tobytes()
+
+
+@pytest.mark.parametrize("rings", [1, 2, 4])
+@pytest.mark.parametrize("case", CASES)
+def test_direct_sim(gpu, lib, oracle, monkeypatch, case, rings):
+    """PG_ALGO=direct (csrc/pg_direct.c): block q goes straight to rank q over
+    its own link and block r is folded from all W copies in one launch per
+    segment batch, each ring part in its ring's order -- bit-exact against the
+    oracle ring for reduce-scatter, all-reduce (out of place and in place) and
+    all-gather, device and host buffers, every segment size and inflight of the
+    ring cases (ragged blocks, count < W, eager sizes)."""
+    monkeypatch.setenv("PG_ALGO", "direct")
+    world, dt, op, count, cb, eager, infl = case
+    xs = [oracle.fill(count, dt, op, 8000 + 5 * r + count) for r in range(world)]
+    want_rs = oracle.ring_reduce_scatter(xs, dt, op, rings)
+    want_ar = oracle.ring_all_reduce(xs, dt, op, rings)
+    want_ag = oracle.ring_all_gather(xs, dt)
+    for on_dev in (True, False):
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, [np.zeros(max(w.size, 1), NP[dt]) for w in want_rs],
+                  count, dt, op, cb, eager, infl, on_dev, rings)
+        for r in range(world):
+            assert got[r][:want_rs[r].size].tobytes() == want_rs[r].tobytes(), (case, "rs", r, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_ALL_REDUCE, xs, [np.zeros(count, NP[dt]) for _ in xs],
+                  count, dt, op, cb, eager, infl, on_dev, rings)
+        for r in range(world):
+            assert got[r].tobytes() == want_ar[r].tobytes(), (case, "ar", r, on_dev)
+        R = [to_dev(gpu, x) for x in xs] if on_dev else [x.copy() for x in xs]
+        ps = (ctypes.c_void_p * world)(*[(ptr(t) if on_dev else t.ctypes.data) for t in R])
+        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, cb, eager, infl, rings) == 0, \
+            pgamd.last_error()
+        for r in range(world):
+            g = to_host(gpu, R[r]) if on_dev else R[r]
+            assert g.tobytes() == want_ar[r].tobytes(), (case, "ar in place", r, on_dev)
+        got = sim(lib, gpu, pgamd.PG_COLL_ALL_GATHER, xs, [np.zeros(max(count * world, 1), NP[dt]) for _ in xs],
+                  count, dt, 0, cb, eager, infl, on_dev, rings)
+        for r in range(world):
+            assert got[r][:want_ag[r].size].tobytes() == want_ag[r].tobytes(), (case, "ag", r, on_dev)
+
+
+def test_direct_large_and_random(gpu, lib, oracle, monkeypatch):
+    """PG_ALGO=direct on a 4-rank 64 Mi-element double sum with the default
+    4 MiB x 4 segments (many batches, both rings), then 60 random shapes."""
+    monkeypatch.setenv("PG_ALGO", "direct")
+    world, count = 4, 1 << 26
+    xs = [oracle.fill(count, 1, 0, 8800 + r) for r in range(world)]
+    want = oracle.ring_reduce_scatter(xs, 1, 0)
+    got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, [np.zeros(w.size, np.float64) for w in want],
+              count, 1, 0, 4 << 20, 4096, 4, True)
+    for r in range(world):
+        assert got[r].tobytes() == want[r].tobytes()
+    del xs, want, got
+    gpu.cuda.empty_cache()
+    rng = np.random.default_rng(99)
+    for i in range(60):
+        world = int(rng.choice([2, 3, 5, 8, 16]))
+        coll = int(rng.integers(3))
+        dt, op = int(rng.integers(2)), int(rng.integers(2))
+        count = int(rng.choice([1, world - 1, world + 1, 97, 4099, 65537, 300007]))
+        cb = int(rng.choice([4, 64, 4096, 1 << 16, 4 << 20]))
+        infl, rings = int(rng.integers(1, 9)), int(rng.integers(1, 5))
+        on_dev = bool(rng.integers(2))
+        xs = [oracle.fill(count, dt, op, 88000 + 31 * i + r) for r in range(world)]
+        if coll == pgamd.PG_COLL_REDUCE_SCATTER:
+            want = oracle.ring_reduce_scatter(xs, dt, op, rings)
+            recvs = [np.zeros(max(w.size, 1), NP[dt]) for w in want]
+        elif coll == pgamd.PG_COLL_ALL_GATHER:
+            want = oracle.ring_all_gather(xs, dt)
+            recvs = [np.zeros(count * world, NP[dt]) for _ in range(world)]
+        else:
+            want = oracle.ring_all_reduce(xs, dt, op, rings)
+            recvs = [np.zeros(count, NP[dt]) for _ in range(world)]
+        got = sim(lib, gpu, coll, xs, recvs, count, dt, op, cb, 0, infl, on_dev, rings)
+        for r in range(world):
+            assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (i, world, coll, dt, op, count, cb, infl,
+                                                                           rings, on_dev, r)

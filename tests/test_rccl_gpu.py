@@ -56,9 +56,11 @@ def _rccl_env(rank, port, split_hosts):
     return env
 
 
-def _worker(rank, world, port, q, rings, chunk_bytes, inflight, cases):
+def _worker(rank, world, port, q, rings, chunk_bytes, inflight, cases, algo):
     os.environ.update(_rccl_env(rank, port, True), PG_RINGS=str(rings), PG_CHUNK_BYTES=str(chunk_bytes),
                       PG_INFLIGHT=str(inflight))
+    if algo:
+        os.environ["PG_ALGO"] = algo
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -139,14 +141,18 @@ def _run(world, target, args_of, timeout=300):
     return results, procs
 
 
-@pytest.mark.parametrize("world,rings,chunk_bytes,inflight", [
-    (2, 2, 4 << 20, 4), (2, 1, 1 << 16, 2), (3, 2, 1 << 18, 4), (4, 4, 1 << 16, 3), (4, 1, 4 << 20, 1)])
-def test_rccl_ring_multiprocess(gpu, world, rings, chunk_bytes, inflight):
-    """The RCCL ring at W = 2, 3, 4 with 1, 2 and 4 rings, small and default
+@pytest.mark.parametrize("world,rings,chunk_bytes,inflight,algo", [
+    (2, 2, 4 << 20, 4, "ring"), (2, 1, 1 << 16, 2, "ring"), (3, 2, 1 << 18, 4, "ring"), (4, 4, 1 << 16, 3, "ring"),
+    (4, 1, 4 << 20, 1, "ring"),
+    (2, 2, 4 << 20, 4, None), (3, 2, 1 << 16, 2, "direct"), (4, 4, 1 << 18, 3, "direct"), (4, 1, 1 << 16, 1, None)])
+def test_rccl_ring_multiprocess(gpu, world, rings, chunk_bytes, inflight, algo):
+    """The RCCL transport at W = 2, 3, 4 with 1, 2 and 4 rings, small and default
     segments, against the oracle ring -- every collective form, host and device
-    buffers, in place, the eager one-shot sizes and config 1's exact shape."""
+    buffers, in place, the eager one-shot sizes and config 1's exact shape.
+    algo: PG_ALGO=ring (the W-1 round ring), direct (one hop per block over
+    every link, csrc/pg_direct.c), None (the default: direct, one host)."""
     cases = CASES if world == 2 else [c for c in CASES if c[3] != 1 << 20]
-    results, procs = _run(world, _worker, lambda r: (rings, chunk_bytes, inflight, cases))
+    results, procs = _run(world, _worker, lambda r: (rings, chunk_bytes, inflight, cases, algo))
     for rank, fails in results:
         assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)
@@ -185,4 +191,95 @@ def test_rccl_duplicate_device_refused_cleanly(gpu):
         assert res[0] == -1, (rank, res)
         assert res[1] < 60.0, (rank, res)
         assert "Duplicate" in res[2] or "invalid usage" in res[2].lower() or "ncclCommInitRank" in res[2], (rank, res)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def _native_worker(rank, world, port, q, store_port):
+    """Our collectives against RCCL's own (torch.distributed, backend nccl =
+    RCCL) on the same inputs: an implementation the oracle's author did not
+    write.  int32 sum and product: bit-exact for reduce-scatter, all-gather and
+    all-reduce (two's-complement wrap is order-independent).  double sum: our
+    result is bit-exact against the oracle ring and within the survey's bound of
+    RCCL's (different fold order)."""
+    os.environ.update(_rccl_env(rank, port, True))
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{store_port}", rank=rank, world_size=world)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) != 0:
+            q.put((rank, ["connect: " + pgamd.last_error()]))
+            return
+        for count in (world * 1000, world * 65536 + 0):
+            for op in (0, 1):
+                xs = [orc.fill(count, 0, op, 4242 + 7 * r + op) for r in range(world)]
+                x = torch.from_numpy(xs[rank]).cuda()
+                rop = dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.PRODUCT
+                ln = count // world
+                ours = torch.empty(ln, dtype=torch.int32, device="cuda")
+                nat = torch.empty(ln, dtype=torch.int32, device="cuda")
+                assert lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), count, 0, op, h) == 0, pgamd.last_error()
+                dist.reduce_scatter_tensor(nat, x, op=rop)
+                torch.cuda.synchronize()
+                if not torch.equal(ours, nat):
+                    fails.append(("rs", count, op))
+                ar = torch.empty(count, dtype=torch.int32, device="cuda")
+                assert lib.pg_all_reduce(x.data_ptr(), ar.data_ptr(), count, 0, op, h) == 0, pgamd.last_error()
+                nat_ar = x.clone()
+                dist.all_reduce(nat_ar, op=rop)
+                torch.cuda.synchronize()
+                if not torch.equal(ar, nat_ar):
+                    fails.append(("ar", count, op))
+            ag = torch.empty(count * world, dtype=torch.int32, device="cuda")
+            assert lib.pg_all_gather(x.data_ptr(), ag.data_ptr(), count, 0, h) == 0, pgamd.last_error()
+            nat_ag = torch.empty_like(ag)
+            dist.all_gather_into_tensor(nat_ag, x)
+            torch.cuda.synchronize()
+            if not torch.equal(ag, nat_ag):
+                fails.append(("ag", count))
+        # double sum: bit-exact against the oracle's ring, within the bound of RCCL's
+        count = world * 100003
+        xs = [orc.fill(count, 1, 0, 5151 + r) for r in range(world)]
+        want = orc.ring_reduce_scatter(xs, 1, 0, 2)[rank]
+        x = torch.from_numpy(xs[rank]).cuda()
+        ours = torch.empty(count // world, dtype=torch.float64, device="cuda")
+        nat = torch.empty_like(ours)
+        sabs = torch.empty_like(ours)
+        assert lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), count, 1, 0, h) == 0, pgamd.last_error()
+        dist.reduce_scatter_tensor(nat, x)
+        dist.reduce_scatter_tensor(sabs, x.abs())
+        torch.cuda.synchronize()
+        if ours.cpu().numpy().tobytes() != want.tobytes():
+            fails.append(("f64 vs oracle",))
+        g = (world - 1) * 2.0 ** -53
+        tol = 2 * g / (1 - g) * sabs
+        if not bool(((ours - nat).abs() <= tol).all()):
+            fails.append(("f64 vs rccl", float((ours - nat).abs().max())))
+        lib.pg_close(h)
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_collectives_match_rccl_native(gpu, world):
+    """An independent pin for the W > 1 output contract: RCCL's own
+    reduce-scatter / all-gather / all-reduce on the same int32 inputs give the
+    same bits (sum and product), and the double sum stays within the survey's
+    tolerance of RCCL's while matching the oracle exactly."""
+    store_port = _free_port()
+    results, procs = _run(world, _native_worker, lambda r: (store_port,))
+    for rank, fails in results:
+        assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)
