@@ -825,7 +825,7 @@ def ring_leg(lib, args, rank, world, transport, sink):
             progress(rank, f"  {transport}: chunk sweep")
             rows = []
             default_cb = int(hd.chunk_bytes)
-            for cb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20):
+            for cb in [1 << e for e in range(16, 29)]:          # 64 KiB .. 256 MiB, every power of two
                 hd.chunk_bytes = cb
                 t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
                 rows.append([payload, rounds, int(hd.inflight), round(t * 1e6, 1), round(payload / t / 1e9, 2),
