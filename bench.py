@@ -267,12 +267,13 @@ def size_leg(lib, rank, world, reps=20):
                          size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4),
                          round(sms * 1e3, 2), round(sgbs / HBM_PEAK_GBS, 4)])
     batches = ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
+    direct = direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     lib.pgk_event_destroy(stamp[0])
     lib.pgk_event_destroy(stamp[1])
     del pool
     torch.cuda.empty_cache()
     return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
-                        "stamped_frac"], "rows": rows, "ring_batches": batches,
+                        "stamped_frac"], "rows": rows, "ring_batches": batches, "direct_batches": direct,
             "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
                       "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
                       "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
@@ -331,6 +332,54 @@ def ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps):
                         "stamped_frac"], "rows": rows,
             "note": "one pgk_reduce_ranges launch = one executor batch (rings ranges of chunk_bytes x inflight), "
                     "double sum; first row = the library defaults"}
+
+
+def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
+    """What one fold of the direct exchange costs (PG_ALGO=direct, the rccl
+    transport's default on one node): a batch of PG_INFLIGHT segments of
+    PG_CHUNK_BYTES of one ring part, folded from the W = 8 copies of the block
+    (7 received + this rank's own) by ONE pgk_reduce_multi launch; traffic
+    (W+1) x chunk x inflight.  Sources rotate over the 4 GiB pool.  double sum."""
+    rows = []
+    dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
+    VP = ctypes.c_void_p
+    for chunk, inflight in ((4 << 20, 4), (1 << 20, 4), (16 << 20, 4), (4 << 20, 8)):
+        rng = chunk * inflight                    # bytes per source per launch
+        slot = 64 << 20
+        sets = SWEEP_POOL // (slot * (nsrc + 1))
+
+        def launch(i, ev=(None, None)):
+            b0 = base + slot * (nsrc + 1) * (i % sets)
+            srcs = (VP * nsrc)(*[b0 + slot * j for j in range(nsrc)])
+            if lib.pgk_reduce_multi_timed(b0 + slot * nsrc, srcs, nsrc, rng // 8, dt, op, sh, ev[0], ev[1]) != 0:
+                raise RuntimeError(pgamd.last_error())
+
+        for i in range(4):
+            launch(i)
+        torch.cuda.synchronize()
+        barrier(world)
+        e0.record(torch.cuda.current_stream())
+        for i in range(reps):
+            launch(i)
+        e1.record(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+        st = []
+        for i in range(8):
+            launch(i, stamp)
+            torch.cuda.synchronize()
+            v = ctypes.c_float()
+            pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
+            st.append(v.value)
+        sms = max_over_ranks(float(np.median(st)), world)
+        traffic = (nsrc + 1) * rng
+        rows.append([chunk, inflight, nsrc, rng, round(ms * 1e3, 2),
+                     round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), round(sms * 1e3, 2),
+                     round(traffic / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
+    return {"columns": ["chunk_bytes", "inflight", "sources", "bytes_per_source", "kernel_us", "frac", "stamped_us",
+                        "stamped_frac"], "rows": rows,
+            "note": "one pgk_reduce_multi launch = one direct-exchange fold (W = 8 sources of chunk_bytes x inflight), "
+                    "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults"}
 
 
 def cpu_baseline(args):

@@ -84,7 +84,7 @@ struct pg_step {
   int64_t recv_off, recv_bytes;
   int64_t red_dst_off, red_src_off, red_elems;
   int32_t red_rev;     /* 1: red_dst = red_src op red_dst (in-place last round) */
-  int32_t reserved;
+  int32_t red_fold;    /* direct plans: 1 = fold block `rank`'s W copies, see below */
 };
 
 /* Reduce-scatter plan for one rank.  Clockwise ring: round k sends block
@@ -113,6 +113,19 @@ PG_API int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
  * uniform = 0: the reduce-scatter partition of `count` (pg_all_reduce). */
 PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform, int rings,
                        struct pg_step *steps, int max_steps);
+
+/* Direct-exchange plan (PG_ALGO=direct) for one rank's reduce-scatter.
+ * Transfer steps (red_elems == 0): send `send_bytes` of SRC at send_off to
+ * rank+send_peer and receive `recv_bytes` from rank+recv_peer into STAGE0 at
+ * recv_off (STAGE0 = W slots of B = ceil(count/world) elements; slot q holds
+ * rank q's copy of block `rank`).  Fold steps (red_fold == 1, after the
+ * transfers of their batch): OUT[red_dst_off ..] (red_elems elements, offsets
+ * in bytes within block `rank`) = x[rank+d] op x[rank+2d] op ... op x[rank]
+ * with d = pg_ring_offset(world, rings, seg), x[q] = slot q of STAGE0 at
+ * red_src_off, x[rank] = SRC at (block offset + red_src_off).  Batches carry
+ * `inflight` segments of chunk_bytes; every rank's groups pair up. */
+PG_API int pg_plan_direct_reduce_scatter(int rank, int world, int count, int datatype, size_t chunk_bytes,
+                                         int inflight, int rings, struct pg_step *steps, int max_steps);
 
 /* Open a handle without a server list: transport LOOPBACK (reference mock
  * semantics for a given rank/world) or SELF (world must be 1).  The device is

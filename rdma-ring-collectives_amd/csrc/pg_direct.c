@@ -24,6 +24,10 @@
  * segments go to a gather area of W block-sized slots, never reused inside a
  * call, so the comm stream never waits for a fold.
  *
+ * The schedule is data: pg_plan_direct_reduce_scatter (pg_plan.c) lists the
+ * transfer and fold steps, so tests/test_plan_gloo.py runs the same plan over
+ * gloo processes without a GPU.
+ *
  * All-gather and the all-reduce's gather half: one group, every rank sending
  * its block (slot) to every peer.
  *
@@ -42,45 +46,6 @@ int pg_direct_applies(const struct pg *pg, int count) {
   return im->algo == PG_ALGO_DIRECT && pg->world_size > 1 && pg->world_size <= DIRECT_MAX_WORLD && count > 0;
 }
 
-/* Segment s of the flat segment list (ring parts in order, each cut into
- * `seg`-element pieces, counted on the FULL block of `full` elements) applied
- * to a block of `len` elements: [*off, *off + *n) inside the block, and the
- * ring part it belongs to.  Returns 0 past the end of the list. */
-struct seglist {
-  int rings;
-  size_t full, seg;
-  int count[PG_MAX_RINGS];      /* segments per part (full block) */
-  int total;
-};
-
-static void seglist_init(struct seglist *sl, size_t full, int rings, size_t seg) {
-  memset(sl, 0, sizeof(*sl));
-  sl->rings = rings;
-  sl->full = full;
-  sl->seg = seg ? seg : 1;
-  for (int g = 0; g < rings; ++g) {
-    size_t po, pl;
-    pg_block_part(full, rings, g, &po, &pl);
-    sl->count[g] = (int)((pl + sl->seg - 1) / sl->seg);
-    sl->total += sl->count[g];
-  }
-}
-
-static int seglist_get(const struct seglist *sl, int s, size_t len, int *part, size_t *off, size_t *n) {
-  int g = 0;
-  while (g < sl->rings && s >= sl->count[g]) s -= sl->count[g++];
-  if (g >= sl->rings) return 0;
-  size_t po, pl;
-  pg_block_part(len, sl->rings, g, &po, &pl);
-  size_t a = (size_t)s * sl->seg, b = a + sl->seg;
-  if (a > pl) a = pl;
-  if (b > pl) b = pl;
-  *part = g;
-  *off = po + a;
-  *n = b - a;
-  return 1;
-}
-
 static int direct_finish(struct pg_impl *im) {
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
@@ -93,7 +58,8 @@ static int direct_finish(struct pg_impl *im) {
 }
 
 /* Reduce-scatter core: block `rank` of the reduction of every rank's `src`
- * (device, count elements) into `out` (device, the block's length). */
+ * (device, count elements) into `out` (device, the block's length), running
+ * the plan of pg_plan_direct_reduce_scatter (pg_plan.c; include/pg_ext.h). */
 static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, int dt, int op) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   const int W = pg->world_size, r = pg->rank;
@@ -101,71 +67,62 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
   size_t boff, blen;
   pg_block_range(count, W, r, &boff, &blen);
   if (pg_ensure(&im->ebuf, &im->ebuf_cap, (size_t)W * full * es)) return -1;
-  char *gat = (char *)im->ebuf;                      /* slot q: rank q's copy of block r */
-  struct seglist sl;
-  size_t seg = pg->chunk_bytes / es;
-  seglist_init(&sl, full, im->rings, seg);
-  const int inflight = pg->inflight > 0 ? pg->inflight : 1;
+  char *gat = (char *)im->ebuf;                      /* STAGE0: slot q = rank q's copy of block r */
+  int n = pg_plan_direct_reduce_scatter(r, W, count, dt, pg->chunk_bytes, pg->inflight, im->rings, NULL, 0);
+  if (n < 0) { pg_set_error("direct: bad plan arguments"); return -1; }
+  if (n > im->steps_cap) {
+    struct pg_step *st = (struct pg_step *)realloc(im->steps, sizeof(*st) * (size_t)n);
+    if (!st) { pg_set_error("direct: out of host memory"); return -1; }
+    im->steps = st;
+    im->steps_cap = n;
+  }
+  pg_plan_direct_reduce_scatter(r, W, count, dt, pg->chunk_bytes, pg->inflight, im->rings, im->steps, n);
+  const struct pg_step *st = im->steps;
   int dsteps[PG_MAX_RINGS];
   for (int g = 0; g < im->rings; ++g) dsteps[g] = pg_ring_offset(W, im->rings, g);
 
   PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
-  int nb = 0;
-  for (int s0 = 0; s0 < sl.total; s0 += inflight, ++nb) {
-    const int s1 = s0 + inflight < sl.total ? s0 + inflight : sl.total;
+  int i = 0, nb = 0;
+  while (i < n) {
+    int j = i;
+    while (j < n && st[j].batch == st[i].batch) ++j;   /* steps [i, j) = one batch */
     if (im->ops->group_start(im)) return -1;
-    for (int k = 1; k < W; ++k) {                    /* peers r+1, r+2, ...: spread over the links */
-      const int q = (r + k) % W;
-      size_t qoff, qlen;
-      pg_block_range(count, W, q, &qoff, &qlen);
-      for (int s = s0; s < s1; ++s) {
-        int part;
-        size_t o, n;
-        if (seglist_get(&sl, s, qlen, &part, &o, &n) && n) {
-          if (im->ops->send(im, src + (qoff + o) * es, n * es, q, im->comm)) return -1;
-          im->stats.bytes_sent += (int64_t)(n * es);
-        }
-        if (seglist_get(&sl, s, blen, &part, &o, &n) && n) {
-          if (im->ops->recv(im, gat + ((size_t)q * full + o) * es, n * es, q, im->comm)) return -1;
-          im->stats.bytes_recv += (int64_t)(n * es);
-        }
-      }
+    for (int t = i; t < j; ++t) {
+      const int q = (r + st[t].send_peer) % W;           /* send_peer == recv_peer in direct plans */
+      if (st[t].send_bytes &&
+          im->ops->send(im, src + st[t].send_off, (size_t)st[t].send_bytes, q, im->comm))
+        return -1;
+      if (st[t].recv_bytes &&
+          im->ops->recv(im, gat + st[t].recv_off, (size_t)st[t].recv_bytes, (r + st[t].recv_peer) % W, im->comm))
+        return -1;
+      im->stats.bytes_sent += st[t].send_bytes;
+      im->stats.bytes_recv += st[t].recv_bytes;
     }
     if (im->ops->group_end(im, im->comm)) return -1;
-    hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
+    hipEvent_t rev = im->recv_ev[nb++ % PG_RECV_EVENTS];
     PG_CHECK_HIP(hipEventRecord(rev, im->comm));
     PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-    /* fold the batch: one multi-source launch per run of segments of one part */
-    int s = s0;
-    while (s < s1) {
-      int part, part2;
-      size_t o, n, o2, n2;
-      seglist_get(&sl, s, blen, &part, &o, &n);
-      int e = s + 1;
-      while (e < s1 && seglist_get(&sl, e, blen, &part2, &o2, &n2) && part2 == part && o2 == o + n) {
-        n += n2;
-        ++e;
+    for (int t = i; t < j; ++t) {
+      if (!st[t].red_fold) continue;
+      const size_t o = (size_t)st[t].red_src_off / es, len = (size_t)st[t].red_elems;
+      const void *srcs[DIRECT_MAX_WORLD];
+      for (int k = 0; k < W; ++k) {
+        const int q = ((r + (k + 1) * dsteps[st[t].seg]) % W + W) % W;   /* k = W-1: q = r */
+        srcs[k] = q == r ? (const void *)(src + (boff + o) * es) : (const void *)(gat + ((size_t)q * full + o) * es);
       }
-      if (n) {
-        const void *srcs[DIRECT_MAX_WORLD];
-        for (int j = 0; j < W; ++j) {
-          const int q = ((r + (j + 1) * dsteps[part]) % W + W) % W;     /* j = W-1: q = r */
-          srcs[j] = q == r ? (const void *)(src + (boff + o) * es) : (const void *)(gat + ((size_t)q * full + o) * es);
-        }
-        void *t0 = NULL, *t1 = NULL;
-        if (im->kt_on) {
-          if (pg_kt_pair(im, &t0, &t1)) return -1;
-          im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * n * es);
-        }
-        if (pgk_reduce_multi_timed(out + o * es, srcs, W, n, dt, op, (void *)im->red, t0, t1)) {
-          pg_set_error("direct: %s", pgk_last_error());
-          return -1;
-        }
-        im->stats.reduce_launches++;
-        im->stats.reduce_elems += (int64_t)n * (W - 1);
+      void *t0 = NULL, *t1 = NULL;
+      if (im->kt_on) {
+        if (pg_kt_pair(im, &t0, &t1)) return -1;
+        im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * len * es);
       }
-      s = e;
+      if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, len, dt, op, (void *)im->red, t0, t1)) {
+        pg_set_error("direct: %s", pgk_last_error());
+        return -1;
+      }
+      im->stats.reduce_launches++;
+      im->stats.reduce_elems += (int64_t)len * (W - 1);
     }
+    i = j;
   }
   return 0;
 }

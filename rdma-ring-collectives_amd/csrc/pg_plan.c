@@ -205,6 +205,120 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
   return n;
 }
 
+/* ---- the direct exchange (PG_ALGO=direct, pg_direct.c) ------------------------
+ * Block r is cut into the ring parts (pg_block_part) and each part into
+ * chunk_elems segments, counted on the FULL block so that every block -- and
+ * so every rank -- has the same flat segment list (a short last block has
+ * empty segments).  Batch b = segments [b*inflight, (b+1)*inflight).  For each
+ * batch: for every peer q = rank+k (k = 1 .. W-1), one transfer step per
+ * segment sending that segment of block q from SRC to q and receiving that
+ * segment of block `rank` from q into slot q of STAGE0 (slots of the full
+ * block); then one fold step per run of the batch's segments inside one part
+ * (red_fold = 1, seg = the part's ring). */
+struct dseg {
+  int rings, total;
+  size_t seg;
+  int count[PG_MAX_RINGS];
+};
+
+static void dseg_init(struct dseg *d, size_t full, int rings, size_t seg) {
+  memset(d, 0, sizeof(*d));
+  d->rings = rings;
+  d->seg = seg ? seg : 1;
+  for (int g = 0; g < rings; ++g) {
+    size_t po, pl;
+    pg_block_part(full, rings, g, &po, &pl);
+    d->count[g] = (int)((pl + d->seg - 1) / d->seg);
+    d->total += d->count[g];
+  }
+}
+
+/* segment s of a block of `len` elements: part and [*off, *off + *n) in the block */
+static void dseg_get(const struct dseg *d, int s, size_t len, int *part, size_t *off, size_t *n) {
+  int g = 0;
+  while (g + 1 < d->rings && s >= d->count[g]) s -= d->count[g++];
+  size_t po, pl;
+  pg_block_part(len, d->rings, g, &po, &pl);
+  size_t a = (size_t)s * d->seg, b = a + d->seg;
+  if (a > pl) a = pl;
+  if (b > pl) b = pl;
+  *part = g;
+  *off = po + a;
+  *n = b - a;
+}
+
+int pg_plan_direct_reduce_scatter(int rank, int world, int count, int datatype, size_t chunk_bytes, int inflight,
+                                  int rings, struct pg_step *steps, int max_steps) {
+  size_t es = plan_elem_size(datatype);
+  if (!es || world < 1 || rank < 0 || rank >= world || count < 0 || rings < 1 || rings > PG_MAX_RINGS) return -1;
+  if (inflight < 1) inflight = 1;
+  const size_t full = ((size_t)count + (size_t)world - 1) / (size_t)world;
+  size_t boff, blen;
+  pg_block_range(count, world, rank, &boff, &blen);
+  struct dseg d;
+  dseg_init(&d, full, rings, chunk_bytes / es);
+  int n = 0, batch = 0;
+  for (int s0 = 0; s0 < d.total; s0 += inflight, ++batch) {
+    const int s1 = s0 + inflight < d.total ? s0 + inflight : d.total;
+    for (int k = 1; k < world; ++k) {
+      const int q = (rank + k) % world;
+      size_t qoff, qlen;
+      pg_block_range(count, world, q, &qoff, &qlen);
+      for (int s = s0; s < s1; ++s) {
+        int part;
+        size_t so, sn, ro, rn;
+        dseg_get(&d, s, qlen, &part, &so, &sn);
+        dseg_get(&d, s, blen, &part, &ro, &rn);
+        if (!sn && !rn) continue;
+        struct pg_step st;
+        memset(&st, 0, sizeof(st));
+        st.batch = batch;
+        st.seg = s;
+        st.send_peer = k;
+        st.recv_peer = k;
+        if (sn) { st.send_buf = PG_BUF_SRC; st.send_off = (int64_t)((qoff + so) * es); st.send_bytes = (int64_t)(sn * es); }
+        if (rn) {
+          st.recv_buf = PG_BUF_STAGE0;
+          st.recv_off = (int64_t)(((size_t)q * full + ro) * es);
+          st.recv_bytes = (int64_t)(rn * es);
+        }
+        put(steps, max_steps, n, &st);
+        ++n;
+      }
+    }
+    int s = s0;
+    while (s < s1) {
+      int part, part2;
+      size_t o, len, o2, len2;
+      dseg_get(&d, s, blen, &part, &o, &len);
+      int e = s + 1;
+      while (e < s1) {
+        dseg_get(&d, e, blen, &part2, &o2, &len2);
+        if (part2 != part || o2 != o + len) break;
+        len += len2;
+        ++e;
+      }
+      if (len) {
+        struct pg_step st;
+        memset(&st, 0, sizeof(st));
+        st.batch = batch;
+        st.seg = part;
+        st.red_fold = 1;
+        st.red_dst_buf = PG_BUF_OUT;
+        st.red_dst_off = (int64_t)(o * es);
+        st.red_src_buf = PG_BUF_STAGE0;
+        st.red_src_off = (int64_t)(o * es);
+        st.red_elems = (int64_t)len;
+        put(steps, max_steps, n, &st);
+        ++n;
+      }
+      s = e;
+    }
+  }
+  if (steps && n > max_steps) return -1;
+  return n;
+}
+
 int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform, int rings,
                        struct pg_step *steps, int max_steps) {
   size_t es = plan_elem_size(datatype);

@@ -41,7 +41,7 @@ class PgStep(ctypes.Structure):
         ("recv_off", ctypes.c_int64), ("recv_bytes", ctypes.c_int64),
         ("red_dst_off", ctypes.c_int64), ("red_src_off", ctypes.c_int64),
         ("red_elems", ctypes.c_int64),
-        ("red_rev", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("red_rev", ctypes.c_int32), ("red_fold", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -85,6 +85,7 @@ _SIGS = {
     # include/pg_ext.h
     "pg_block_range": (_I, [_I, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "pg_plan_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _SZ, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
+    "pg_plan_direct_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_block_part": (_I, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "pg_ring_offset": (_I, [_I, _I, _I]),
@@ -180,6 +181,17 @@ def plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max=4096, inf
         raise ValueError("pg_plan_reduce_scatter: bad arguments")
     arr = (PgStep * max(n, 1))()
     m = lib.pg_plan_reduce_scatter(rank, world, count, dt, chunk_bytes, eager_max, inflight, rings, alias, arr, n)
+    assert m == n
+    return [arr[i].as_dict() for i in range(n)]
+
+
+def plan_direct_reduce_scatter(rank, world, count, dt, chunk_bytes, inflight=4, rings=2):
+    lib = load()
+    n = lib.pg_plan_direct_reduce_scatter(rank, world, count, dt, chunk_bytes, inflight, rings, None, 0)
+    if n < 0:
+        raise ValueError("pg_plan_direct_reduce_scatter: bad arguments")
+    arr = (PgStep * max(n, 1))()
+    m = lib.pg_plan_direct_reduce_scatter(rank, world, count, dt, chunk_bytes, inflight, rings, arr, n)
     assert m == n
     return [arr[i].as_dict() for i in range(n)]
 

@@ -1,8 +1,8 @@
 /* tests/c/plan_fuzz.c -- the ring planner (csrc/pg_plan.c, pure C) under
  * AddressSanitizer + UndefinedBehaviorSanitizer: every shape in the grid below
  * is planned for every rank, in one to four rings, reduce-scatter (plain and
- * in place) and all-gather, and every offset a step names must lie inside the
- * buffer it names.  Built and run by tests/test_plan_sanitize.py.  Exit 0 = ok. */
+ * in place), the direct exchange and all-gather, and every offset a step names
+ * must lie inside the buffer it names.  Built and run by tests/test_plan_sanitize.py.  Exit 0 = ok. */
 #include <stdio.h>
 #include <stdlib.h>
 #include "pg.h"
@@ -38,6 +38,23 @@ int main(void) {
                     }
                     total += n;
                     free(st);
+                    if (!alias && !eager) {           /* the direct exchange (no alias / eager knobs) */
+                      n = pg_plan_direct_reduce_scatter(r, W, counts[ci], dt, cbs[cbi], infl, rings, NULL, 0);
+                      if (n < 0) return 7;
+                      st = malloc(sizeof(*st) * (n ? n : 1));
+                      if (pg_plan_direct_reduce_scatter(r, W, counts[ci], dt, cbs[cbi], infl, rings, st, n) != n) return 8;
+                      size_t boff, blen;
+                      pg_block_range(counts[ci], W, r, &boff, &blen);
+                      for (int i = 0; i < n; ++i) {
+                        if (st[i].send_bytes && (size_t)(st[i].send_off + st[i].send_bytes) > counts[ci] * es) return 9;
+                        if (st[i].recv_bytes && (size_t)(st[i].recv_off + st[i].recv_bytes) > (size_t)W * blk * es) return 10;
+                        if (st[i].red_fold && ((size_t)st[i].red_dst_off + st[i].red_elems * es > blen * es ||
+                                               (size_t)st[i].red_src_off + st[i].red_elems * es > blk * es))
+                          return 11;
+                      }
+                      total += n;
+                      free(st);
+                    }
                     n = pg_plan_all_gather(r, W, counts[ci], dt, alias, rings, NULL, 0);
                     st = malloc(sizeof(*st) * (n ? n : 1));
                     pg_plan_all_gather(r, W, counts[ci], dt, alias, rings, st, n);

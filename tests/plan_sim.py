@@ -44,6 +44,29 @@ def _view(bufs, which, off, nbytes):
     return b[off:off + nbytes]
 
 
+def direct_fold(bufs, s, rank, world, dt, op):
+    """A fold step of a direct plan (include/pg_ext.h): OUT = x[r+d] op x[r+2d]
+    op ... op x[r], x[q] = slot q of STAGE0, x[r] = this rank's own block in SRC;
+    bufs["ctx"] = (rings, full block elements, block offset)."""
+    rings, full, boff = bufs["ctx"]
+    es = 4 if dt == 0 else 8
+    n = s["red_elems"] * es
+    d = pgamd.ring_offset(world, rings, s["seg"])
+    acc = None
+    for k in range(world):
+        q = (rank + (k + 1) * d) % world
+        if q == rank:
+            x = _view(bufs, pgamd.PG_BUF_SRC, boff * es + s["red_src_off"], n)
+        else:
+            x = _view(bufs, pgamd.PG_BUF_STAGE0, q * full * es + s["red_src_off"], n)
+        x = x.view(NP[dt])
+        if acc is None:
+            acc = x.copy()
+        else:
+            np_reduce(acc, x, op)
+    _view(bufs, s["red_dst_buf"], s["red_dst_off"], n).view(NP[dt])[:] = acc
+
+
 def run_plans(plans, bufs_per_rank, dt, op):
     """Execute every rank's step list.  bufs_per_rank[r][PG_BUF_*] = uint8 arrays.
     A step runs once all its receives are available; sends snapshot the bytes
@@ -92,7 +115,9 @@ def run_plans(plans, bufs_per_rank, dt, op):
                     assert msg.size == s["recv_bytes"], (r, s, msg.size)
                     _view(bufs, s["recv_buf"], s["recv_off"], s["recv_bytes"])[:] = msg
             for s in batch:
-                if s["red_elems"]:
+                if s.get("red_fold"):
+                    direct_fold(bufs, s, r, world, dt, op)
+                elif s["red_elems"]:
                     d = _view(bufs, s["red_dst_buf"], s["red_dst_off"], s["red_elems"] * es).view(NP[dt])
                     src = _view(bufs, s["red_src_buf"], s["red_src_off"], s["red_elems"] * es).view(NP[dt])
                     np_reduce(d, src, op, s.get("red_rev", 0))
@@ -144,3 +169,19 @@ def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, ring
     agbufs = [{pgamd.PG_BUF_OUT: bufs[r][pgamd.PG_BUF_SRC]} for r in range(world)]
     run_plans(plans, agbufs, dt, 0)
     return [agbufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)]
+
+
+def direct_reduce_scatter(sends, dt, op, chunk_bytes, inflight=4, rings=2):
+    """PG_ALGO=direct: every rank's pg_plan_direct_reduce_scatter steps run
+    together (one hop per block over every link, folds in ring order)."""
+    world, count = len(sends), sends[0].size
+    es = 4 if dt == 0 else 8
+    full = -(-count // world) if count else 0
+    plans, bufs = [], []
+    for r in range(world):
+        plans.append(pgamd.plan_direct_reduce_scatter(r, world, count, dt, chunk_bytes, inflight, rings))
+        off, ln = pgamd.block_range(count, world, r)
+        bufs.append({pgamd.PG_BUF_SRC: sends[r].copy().view(np.uint8), pgamd.PG_BUF_OUT: np.zeros(ln * es, np.uint8),
+                     pgamd.PG_BUF_STAGE0: np.zeros(world * full * es, np.uint8), "ctx": (rings, full, off)})
+    run_plans(plans, bufs, dt, op)
+    return [bufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)]

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import pgamd
-from plan_sim import ring_all_gather, ring_all_reduce, ring_reduce_scatter
+from plan_sim import direct_reduce_scatter, ring_all_gather, ring_all_reduce, ring_reduce_scatter
 
 
 def inputs(oracle, world, count, dt, op, seed):
@@ -180,3 +180,41 @@ def test_in_place_last_round_keeps_arrival_first(rings):
             if s["red_rev"]:
                 assert s["red_dst_buf"] == pgamd.PG_BUF_OUT and s["red_src_buf"] in (pgamd.PG_BUF_STAGE0,
                                                                                       pgamd.PG_BUF_STAGE1)
+
+
+@pytest.mark.parametrize("rings", [1, 2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+def test_direct_plan_matches_oracle(oracle, world, rings):
+    """pg_plan_direct_reduce_scatter (PG_ALGO=direct) executed for every rank
+    at once in numpy: one hop per block, every rank's groups pair up (run_plans
+    asserts no deadlock and no unconsumed message) and the ring-order folds give
+    the oracle ring's bits, ragged and tiny counts included."""
+    for dt, op, count, cb, infl in ((0, 0, 1000, 64, 2), (1, 0, 4099, 256, 4), (1, 1, 77, 8, 1), (0, 1, 3, 4, 3),
+                                    (1, 0, world * 8 + 1, 16, 1), (0, 0, 65537, 4096, 4)):
+        xs = [oracle.fill(count, dt, op, 7000 + 13 * r + count) for r in range(world)]
+        want = oracle.ring_reduce_scatter(xs, dt, op, rings)
+        got = direct_reduce_scatter(xs, dt, op, cb, infl, rings)
+        for r in range(world):
+            assert got[r].tobytes() == want[r].tobytes(), (world, rings, dt, op, count, cb, infl, r)
+
+
+def test_direct_plan_shape():
+    """Every batch of a direct plan: transfers to/from the same peer offset,
+    sends from SRC, receives into STAGE0 slot q, then the batch's folds; the
+    bytes a rank sends equal its input minus its own block."""
+    world, count, es = 4, 1000, 8
+    for r in range(world):
+        st = pgamd.plan_direct_reduce_scatter(r, world, count, 1, 64 * es, 2, 2)
+        off, ln = pgamd.block_range(count, world, r)
+        assert sum(s["send_bytes"] for s in st) == (count - ln) * es
+        assert sum(s["recv_bytes"] for s in st) == ln * (world - 1) * es
+        assert sum(s["red_elems"] for s in st if s["red_fold"]) == ln
+        for s in st:
+            if s["red_fold"]:
+                assert not s["send_bytes"] and not s["recv_bytes"] and s["red_dst_buf"] == pgamd.PG_BUF_OUT
+            else:
+                assert s["send_peer"] == s["recv_peer"] and 1 <= s["send_peer"] < world
+                q = (r + s["recv_peer"]) % world
+                if s["recv_bytes"]:
+                    assert s["recv_buf"] == pgamd.PG_BUF_STAGE0
+                    assert q * 250 * es <= s["recv_off"] < (q + 1) * 250 * es

@@ -1,4 +1,4 @@
-"""The N>1 path on CPU: world_size 2 and 4 over torch.distributed gloo.
+"""The N>1 path on CPU: world_size 2, 4 and 5 over torch.distributed gloo, ring and direct schedules.
 
 Each process asks libpg_amd.so for ITS rank's plan (pg_plan_reduce_scatter /
 pg_plan_all_gather, the schedule the GPU executor runs) and executes it with
@@ -29,14 +29,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, algo="ring"):
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd"), str(ROOT / "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import pgamd
         from oracle.pyoracle import Oracle
-        from plan_sim import NP, np_reduce
+        from plan_sim import NP, direct_fold, np_reduce
         orc = Oracle()
         fails = []
         for (dt, op, count, cb, infl), rings in itertools.product(
@@ -50,7 +50,12 @@ def _worker(rank, world, port, q):
             bmax = rings * -(-blk // rings) * es          # staging: R * ceil(B/R) elements
             bufs = {pgamd.PG_BUF_SRC: xs[rank].copy().view(np.uint8), pgamd.PG_BUF_OUT: np.zeros(ln * es, np.uint8),
                     pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)}
-            steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl, rings=rings)
+            if algo == "direct":          # one hop per block over every peer (pg_plan_direct_reduce_scatter)
+                bufs[pgamd.PG_BUF_STAGE0] = np.zeros(world * blk * es, np.uint8)
+                bufs["ctx"] = (rings, blk, off)
+                steps = pgamd.plan_direct_reduce_scatter(rank, world, count, dt, cb, infl, rings)
+            else:
+                steps = pgamd.plan_reduce_scatter(rank, world, count, dt, cb, 0, infl, rings=rings)
             i = 0
             while i < len(steps):
                 j = i
@@ -72,7 +77,9 @@ def _worker(rank, world, port, q):
                     else:
                         r_.wait()
                 for s in steps[i:j]:
-                    if s["red_elems"]:
+                    if s["red_fold"]:
+                        direct_fold(bufs, s, rank, world, dt, op)
+                    elif s["red_elems"]:
                         n = s["red_elems"] * es
                         d = bufs[s["red_dst_buf"]][s["red_dst_off"]:s["red_dst_off"] + n].view(NP[dt])
                         src = bufs[s["red_src_buf"]][s["red_src_off"]:s["red_src_off"] + n].view(NP[dt])
@@ -86,12 +93,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4, 5])
-def test_ring_plan_over_gloo(world):
+@pytest.mark.parametrize("world,algo", [(2, "ring"), (4, "ring"), (5, "ring"), (2, "direct"), (4, "direct"),
+                                        (5, "direct")])
+def test_ring_plan_over_gloo(world, algo):
+    """algo "ring": pg_plan_reduce_scatter; "direct": pg_plan_direct_reduce_scatter
+    (every send goes to its block's owner; the folds follow the ring order)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, algo)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=300) for _ in range(world)]

@@ -71,6 +71,9 @@ static const V kV[] = {
     {"reduce 256x1", 4, 256, 1},     {"reduce 256x2", 4, 256, 2},
     {"reduce 1024x1", 4, 1024, 1},   {"reduce 1024x4", 4, 1024, 4},
     {"reduce 512x4", 4, 512, 4},
+    {"reduce 128x2", 4, 128, 2},     {"reduce 128x4", 4, 128, 4},
+    {"reduce 256x4", 4, 256, 4},     {"reduce 512x1", 4, 512, 1},
+    {"reduce 768x1", 4, 768, 1},     {"reduce 1024x2", 4, 1024, 2},
 };
 
 template <int B, int U>
@@ -106,6 +109,12 @@ extern "C" int edge_launch(int v, double* d, const double* s, size_t n, void* st
     case 1024 * 16 + 1: go<1024, 1>(x.kind, d, s, n, st, a, b); break;
     case 1024 * 16 + 4: go<1024, 4>(x.kind, d, s, n, st, a, b); break;
     case 512 * 16 + 4: go<512, 4>(x.kind, d, s, n, st, a, b); break;
+    case 128 * 16 + 2: go<128, 2>(x.kind, d, s, n, st, a, b); break;
+    case 128 * 16 + 4: go<128, 4>(x.kind, d, s, n, st, a, b); break;
+    case 256 * 16 + 4: go<256, 4>(x.kind, d, s, n, st, a, b); break;
+    case 512 * 16 + 1: go<512, 1>(x.kind, d, s, n, st, a, b); break;
+    case 768 * 16 + 1: go<768, 1>(x.kind, d, s, n, st, a, b); break;
+    case 1024 * 16 + 2: go<1024, 2>(x.kind, d, s, n, st, a, b); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

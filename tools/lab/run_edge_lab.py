@@ -45,6 +45,12 @@ pgamd.check(lib.pgk_event_create(ctypes.byref(ev[1])), "event")
 TRAFFIC = {0: 0, 1: 2, 2: 1, 3: 2, 4: 3}
 KIND = {"empty": 0, "read": 1, "write": 2, "copy": 3, "reduce": 4}
 variants = [-1] + [v for v in range(32) if lab.edge_name(v)]
+B2B = "--b2b" in sys.argv       # events bracketing back-to-back launches (the bench's kernel_us) instead of stamps
+if B2B:
+    sys.argv.remove("--b2b")
+if "--reduce-only" in sys.argv:
+    sys.argv.remove("--reduce-only")
+    variants = [v for v in variants if v < 0 or lab.edge_name(v).decode().startswith("reduce")]
 
 
 def name(v):
@@ -64,6 +70,20 @@ for size in sizes:
     times = {v: [] for v in variants}
     for rnd in range(4):
         for v in variants:
+            if B2B:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for i in range(13):
+                    if i == 1:
+                        e0.record()
+                    d = base + 2 * size * (k % pairs)
+                    k += 1
+                    rc = (lib.pgk_reduce(d, d + size, n, 1, 0, sh) if v < 0
+                          else lab.edge_launch(v, d, d + size, n, sh, None, None))
+                    assert rc == 0, (v, rc)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) * 1e3 / 12)
+                continue
             for i in range(6):
                 d = base + 2 * size * (k % pairs)
                 k += 1
@@ -75,7 +95,8 @@ for size in sizes:
                 pgamd.check(lib.pgk_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)), "elapsed")
                 if i >= 1:
                     times[v].append(ms.value * 1e3)
-    print(f"== {size >> 20} MiB per operand (kernel-stamped us: median / min) ==", flush=True)
+    print(f"== {size >> 20} MiB per operand ({'back-to-back, events / launch' if B2B else 'kernel-stamped'} us: "
+          "median / min) ==", flush=True)
     for v in variants:
         m = statistics.median(times[v])
         med[(v, size)] = m
