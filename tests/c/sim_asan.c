@@ -70,16 +70,22 @@ int main(void) {
     for (int coll = 0; coll < 3; ++coll)
       for (int rings = 1; rings <= 4; rings += (rings == 2 ? 2 : 1))
         for (int on_dev = 0; on_dev < 2; ++on_dev)
-          for (int eager = 0; eager <= 4096; eager += 4096) {
+          for (int eager = 0; eager <= 8192; eager += 4096) {
+            /* eager 0 / 4096: the ring (and the eager one-shot); 8192 stands for
+             * the direct exchange (PG_ALGO=direct, eager off) */
             const int *s = shapes[i];
-            int rc = run_case(s[0], coll, s[1], s[2], s[3], (size_t)s[4], (size_t)eager, s[5], rings, on_dev);
+            const int direct = eager == 8192;
+            setenv("PG_ALGO", direct ? "direct" : "ring", 1);
+            int rc = run_case(s[0], coll, s[1], s[2], s[3], (size_t)s[4], direct ? 0 : (size_t)eager, s[5], rings,
+                              on_dev);
             ++cases;
             if (rc) {
-              fprintf(stderr, "case W=%d count=%d dt=%d op=%d coll=%d rings=%d dev=%d eager=%d: %d\n", s[0], s[1],
-                      s[2], s[3], coll, rings, on_dev, eager, rc);
+              fprintf(stderr, "case W=%d count=%d dt=%d op=%d coll=%d rings=%d dev=%d eager=%d direct=%d: %d\n", s[0],
+                      s[1], s[2], s[3], coll, rings, on_dev, eager, direct, rc);
               ++fails;
             }
           }
+  unsetenv("PG_ALGO");
   /* the host-operand reduce */
   size_t n = (5u << 20) + 7;
   double *d = malloc(n * 8), *s = malloc(n * 8), *w = malloc(n * 8);

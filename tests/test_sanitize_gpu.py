@@ -1,8 +1,9 @@
 """The host side of the ring path under AddressSanitizer + UndefinedBehavior-
 Sanitizer, on the GPU (tests/c/sim_asan.c, built by tests/c/Makefile.asan from
-__graft_entry__.build()): plan, executor, staging hooks, eager one-shot,
-threads transport and the host-operand reduce over 288 cases (1, 2 and 4
-rings), every result bit for bit against the oracle's ring simulator.  Host code only: the kernels are
+__graft_entry__.build()): plan, executor, staging hooks, eager one-shot, the
+direct exchange (PG_ALGO=direct), threads transport and the host-operand
+reduce over 432 cases (1, 2 and 4 rings), every result bit for bit against the
+oracle's ring simulator.  Host code only: the kernels are
 built without sanitizers (GPU sanitizers are not available on this pool)."""
 import os
 import pathlib
