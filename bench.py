@@ -65,10 +65,10 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the RCCL ring leg at N > 1")
     ap.add_argument("--ring-steps", type=int, default=3)
     ap.add_argument("--ring-timeout", type=float, default=300.0, help="watchdog for the ring leg (s)")
-    ap.add_argument("--transports", default="xgmi,xgmi_push,rccl",
+    ap.add_argument("--transports", default="xgmi,xgmi_push,xgmi_read,rccl",
                     help="ring-leg transports, comma separated (rccl last, so a stalled RCCL leg cannot take "
-                         "the tested xgmi rows with it; xgmi_push = PG_TRANSPORT=xgmi with PG_XGMI_MODE=push, "
-                         "timed call only)")
+                         "the tested xgmi rows with it; xgmi = the library default, PG_XGMI_MODE=auto; "
+                         "xgmi_push / xgmi_read = the mode forced, correctness probe and timed call only)")
     ap.add_argument("--ring-div", type=int, default=1,
                     help="divide the ring-leg element counts (one-GPU rehearsals over RCCL's socket transport "
                          "only; the driver's runs keep the BASELINE shapes)")
@@ -787,10 +787,10 @@ def ring_leg(lib, args, rank, world, transport, sink):
     hosts = " ".join(["127.0.0.1"] * world).encode()
     os.environ["PG_RANK"] = str(rank)
     os.environ["PG_TRANSPORT"] = "xgmi" if transport.startswith("xgmi") else transport
-    os.environ["PG_XGMI_MODE"] = "push" if transport == "xgmi_push" else "read"
+    os.environ["PG_XGMI_MODE"] = {"xgmi_push": "push", "xgmi_read": "read"}.get(transport, "auto")
     os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) +
-                                {"rccl": 17, "xgmi": 19, "xgmi_push": 21}[transport])
-    core_only = transport == "xgmi_push"       # the correctness probe and the timed call
+                                {"rccl": 17, "xgmi": 19, "xgmi_push": 21, "xgmi_read": 23}[transport])
+    core_only = transport in ("xgmi_push", "xgmi_read")    # the correctness probe and the timed call
     h = ctypes.c_void_p()
     progress(rank, f"  {transport}: connect_process_group")
     if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
@@ -799,8 +799,17 @@ def ring_leg(lib, args, rank, world, transport, sink):
         hd = pgamd.head(h)
         res = {"workload": cfg, "transport": {
             "rccl": "RCCL point-to-point over xGMI (PG_ALGO default: direct one-hop exchange on one node)",
-            "xgmi": "direct peer reads (HIP IPC) over xGMI, ring fold order",
-            "xgmi_push": "each block written to its owner over xGMI (HIP IPC), folded locally in ring order"}[transport]}
+            "xgmi": "direct peer access (HIP IPC) over xGMI, ring fold order; read or push chosen by the library's "
+                    "connect-time link probe (PG_XGMI_MODE=auto)",
+            "xgmi_read": "direct peer reads (HIP IPC) over xGMI, ring fold order (PG_XGMI_MODE=read)",
+            "xgmi_push": "each block written to its owner over xGMI (HIP IPC), folded locally in ring order "
+                         "(PG_XGMI_MODE=push)"}[transport]}
+        if transport == "xgmi":
+            push, rg, wg = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+            if lib.pgx_xgmi_mode(h, ctypes.byref(push), ctypes.byref(rg), ctypes.byref(wg)) == 0:
+                res["mode"] = {"chosen": "push" if push.value else "read", "probe_read_gbs": round(rg.value, 1),
+                               "probe_write_gbs": round(wg.value, 1),
+                               "rule": "push when all-links write >= 1.15 x all-links read (32 MiB probe at connect)"}
         if os.environ.get("PG_BENCH_ONE_GPU") == "1":
             res["rehearsal"] = ("all ranks share one GPU; rccl runs over RCCL's socket transport on loopback "
                                 "(NCCL_HOSTID per rank), xgmi's links are the one device's HBM: rates are not a node's")

@@ -196,6 +196,14 @@ PG_API int pgx_boot_selftest(const char *serverlist, int rank, int port, int val
  * 1e9 bytes/s moved by this rank.  bytes: a multiple of 4 KiB. */
 PG_API int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs);
 
+/* xgmi transport: the reduce-scatter mode in use (*push: 1 = each rank writes
+ * every peer's block to it, 0 = each rank reads its block from every peer).
+ * PG_XGMI_MODE=auto (the default) chose it at connect time with the link
+ * probe above (32 MiB, all links at once): push when pushed bytes moved >= 15%
+ * faster than pulled ones; *read_gbs / *write_gbs are that probe's medians over
+ * ranks (0 when the mode was forced with PG_XGMI_MODE=read|push). */
+PG_API int pgx_xgmi_mode(void *pg_handle, int *push, double *read_gbs, double *write_gbs);
+
 /* Last error message of the calling thread ("" if none). */
 PG_API const char *pg_last_error(void);
 

@@ -90,6 +90,7 @@ _SIGS = {
     "pg_block_part": (_I, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "pg_ring_offset": (_I, [_I, _I, _I]),
     "pgx_xgmi_link_probe": (_I, [_VP, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
+    "pgx_xgmi_mode": (_I, [_VP, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "pg_connect_local": (_I, [_I, _I, _I, ctypes.POINTER(_VP)]),
     "pgx_sim_run": (_I, [_I, _I, ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _I, _I, _SZ, _SZ, _I, _I]),
     "pg_get_stats": (_I, [_VP, ctypes.POINTER(PgStats)]),

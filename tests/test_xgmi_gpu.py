@@ -65,6 +65,11 @@ def _worker(rank, world, port, q, oneshot_max, zero_copy="1", rings=2, mode="rea
             return
         hd = pgamd.head(h)
         assert (hd.rank, hd.world_size, hd.transport) == (rank, world, pgamd.PG_TRANSPORT_XGMI)
+        if os.environ.get("PG_XGMI_MODE") is None:        # auto: chosen at connect by the link probe
+            push, rg, wg = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+            assert lib.pgx_xgmi_mode(h, ctypes.byref(push), ctypes.byref(rg), ctypes.byref(wg)) == 0
+            assert push.value in (0, 1) and rg.value > 0 and wg.value > 0
+            assert push.value == (wg.value >= 1.15 * rg.value)
         NP = {0: np.int32, 1: np.float64}
         for i, (coll, dt, op, count, on_dev, in_place) in enumerate(CASES):
             if on_dev == "mixed":
@@ -173,11 +178,13 @@ def test_xgmi_push_without_shm_page_reads(gpu, world):
     _run_workers(world, (1 << 20, "1", 2, "push", {"PG_NO_SHM_BARRIER": "1"}))
 
 
-def test_default_transport_is_xgmi_on_one_node(gpu):
-    """No PG_TRANSPORT, every server-list entry the same host, W <= 16: the
-    xgmi transport (pg_default_transport); the worker asserts the handle's
-    transport and runs every case against the oracle."""
-    _run_workers(2, (1 << 20, "1", 2, "read", {"PG_TRANSPORT": None}))
+@pytest.mark.parametrize("world", [2, 4])
+def test_default_transport_is_xgmi_on_one_node(gpu, world):
+    """No PG_TRANSPORT and no PG_XGMI_MODE, every server-list entry the same
+    host, W <= 16: the xgmi transport (pg_default_transport) with the mode the
+    connect-time link probe chose (PG_XGMI_MODE=auto); the worker asserts the
+    transport and the probe's rule, and runs every case against the oracle."""
+    _run_workers(world, (1 << 20, "1", 2, "read", {"PG_TRANSPORT": None, "PG_XGMI_MODE": None}))
 
 
 def _grow_worker(rank, world, port, q):
