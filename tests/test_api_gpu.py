@@ -9,6 +9,7 @@
 """
 import ctypes
 import itertools
+import pathlib
 import socket
 
 import numpy as np
@@ -413,35 +414,61 @@ def test_nan_payloads_all_reduce_matches_reduce_scatter(gpu, lib, oracle, world,
             assert ar_in[r][off:off + ln].tobytes() == rs[r][:ln].tobytes(), (world, rings, op, r, "in place")
 
 
+def _slow_producer_run(lib, torch, oracle, coll, world=4, count=300007):
+    xs = [oracle.fill(count, 1, 0, 9300 + r) for r in range(world)]
+    staged = [to_dev(torch, x) for x in xs]
+    S = [torch.zeros(count, dtype=torch.float64, device="cuda") for _ in xs]
+    n_out = count * world if coll == pgamd.PG_COLL_ALL_GATHER else count
+    R = [torch.zeros(n_out, dtype=torch.float64, device="cuda") for _ in xs]
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)                   # keep the null stream busy ...
+    for s_, st_ in zip(S, staged):
+        s_.copy_(st_)                                # ... and produce the inputs behind it
+    sp = (ctypes.c_void_p * world)(*[ptr(t) for t in S])
+    rp = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
+    assert lib.pgx_sim_run(world, coll, sp, rp, count, 1, 0, 1 << 16, 4096, 4, 2) == 0, pgamd.last_error()
+    if coll == pgamd.PG_COLL_REDUCE_SCATTER:
+        want = oracle.ring_reduce_scatter(xs, 1, 0, 2)
+    elif coll == pgamd.PG_COLL_ALL_REDUCE:
+        want = oracle.ring_all_reduce(xs, 1, 0, 2)
+    else:
+        want = oracle.ring_all_gather(xs, 1)
+    return [to_host(torch, R[r])[:want[r].size].tobytes() == want[r].tobytes() for r in range(world)]
+
+
+def test_device_input_behind_slow_producer_needs_the_wait(gpu, lib, oracle, monkeypatch):
+    """The same sequence with the entry wait switched off (test hook
+    PG_TEST_SKIP_PRODUCER_WAIT=1, read once per process: run in a child) gives
+    wrong results: the non-blocking ring streams read the inputs before the
+    null stream has written them.  So the wait is what the test above passes on."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = [sys.argv[1], sys.argv[1] + '/rdma-ring-collectives_amd', sys.argv[1] + '/tests']\n"
+        "import torch, pgamd\n"
+        "from oracle.pyoracle import Oracle\n"
+        "import test_api_gpu as t\n"
+        "torch.cuda.set_device(0)\n"
+        "ok = t._slow_producer_run(pgamd.load(), torch, Oracle(), pgamd.PG_COLL_REDUCE_SCATTER)\n"
+        "print('RESULT', sum(ok), len(ok))\n")
+    import os
+    env = dict(os.environ, PG_TEST_SKIP_PRODUCER_WAIT="1")
+    root = str(pathlib.Path(__file__).resolve().parents[1])
+    r = subprocess.run([sys.executable, "-c", code, root], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1]
+    good, total = map(int, line.split()[1:])
+    assert good < total, "without the producer wait every rank still matched: the wait would be unnecessary"
+
+
 def test_device_input_behind_slow_producer(gpu, lib, oracle):
     """The entry wait (pg_wait_producers): the caller writes its device input
     on the null stream behind a long-running kernel and calls the collective at
     once.  The ring streams are non-blocking, so without the event wait they
-    would send the old contents; with it every result matches the oracle."""
-    torch = gpu
-    world, count = 4, 300007
+    would send the old contents (see the test above); with it every result
+    matches the oracle."""
     for coll in (pgamd.PG_COLL_REDUCE_SCATTER, pgamd.PG_COLL_ALL_REDUCE, pgamd.PG_COLL_ALL_GATHER):
-        xs = [oracle.fill(count, 1, 0, 9300 + r) for r in range(world)]
-        staged = [to_dev(torch, x) for x in xs]
-        S = [torch.zeros(count, dtype=torch.float64, device="cuda") for _ in xs]
-        n_out = count * world if coll == pgamd.PG_COLL_ALL_GATHER else count
-        R = [torch.zeros(n_out, dtype=torch.float64, device="cuda") for _ in xs]
-        torch.cuda.synchronize()
-        torch.cuda._sleep(200_000_000)                   # keep the null stream busy ...
-        for s_, st_ in zip(S, staged):
-            s_.copy_(st_)                                # ... and produce the inputs behind it
-        sp = (ctypes.c_void_p * world)(*[ptr(t) for t in S])
-        rp = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
-        assert lib.pgx_sim_run(world, coll, sp, rp, count, 1, 0, 1 << 16, 4096, 4, 2) == 0, pgamd.last_error()
-        if coll == pgamd.PG_COLL_REDUCE_SCATTER:
-            want = oracle.ring_reduce_scatter(xs, 1, 0, 2)
-        elif coll == pgamd.PG_COLL_ALL_REDUCE:
-            want = oracle.ring_all_reduce(xs, 1, 0, 2)
-        else:
-            want = oracle.ring_all_gather(xs, 1)
-        for r in range(world):
-            got = to_host(torch, R[r])
-            assert got[:want[r].size].tobytes() == want[r].tobytes(), (coll, r)
+        assert all(_slow_producer_run(lib, gpu, oracle, coll)), coll
 
 
 @pytest.mark.parametrize("on_dev", [True, False])
