@@ -14,10 +14,10 @@ tools/gpu_step.sh latency 300 python tools/latency.py --world 2 --transport xgmi
 tools/gpu_step.sh latency_rccl 300 python tools/latency.py --world 2 --transport rccl --out gpurun_out/latency_rccl.csv
 PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-sizes \
-  --transports xgmi,xgmi_push,rccl --ring-div 4 --ring-timeout 350
+  --transports xgmi,xgmi_push,xgmi_read,rccl --ring-div 4 --ring-timeout 350
 PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n4 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
   --master-addr 127.0.0.1 --master-port 29543 bench.py --gpus 4 --steps 10 --warmup 2 --no-sizes \
-  --transports xgmi,xgmi_push,rccl --ring-div 4 --ring-timeout 450
+  --transports xgmi,xgmi_push,xgmi_read,rccl --ring-div 4 --ring-timeout 450
 PG_BENCH_ONE_GPU=1 tools/gpu_step.sh bench_n8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
   --master-addr 127.0.0.1 --master-port 29553 bench.py --gpus 8 --steps 10 --warmup 2 --no-sizes \
-  --transports xgmi,xgmi_push,rccl --ring-div 8 --ring-timeout 550
+  --transports xgmi,xgmi_push,xgmi_read,rccl --ring-div 8 --ring-timeout 550
