@@ -100,7 +100,7 @@ struct pg_step {
  * staging blocks hold R*ceil(B/R) elements).
  * out_aliases_src: OUT is block `rank` of SRC (in-place all-reduce).  Returns
  * the number of steps written (or needed, when steps == NULL), -1 on bad
- * arguments. */
+ * arguments or a chunk_bytes so small that the plan would exceed 2^28 steps. */
 PG_API int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
                            size_t chunk_bytes, size_t eager_max, int inflight, int rings,
                            int out_aliases_src, struct pg_step *steps, int max_steps);

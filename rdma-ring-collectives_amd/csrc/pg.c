@@ -438,7 +438,7 @@ static int plan_into(struct pg_impl *im, int is_rs, int count, int dt, int alias
   int n = is_rs ? pg_plan_reduce_scatter(pg->rank, pg->world_size, count, dt, pg->chunk_bytes,
                                          pg->eager_max, pg->inflight, im->rings, alias, NULL, 0)
                 : pg_plan_all_gather(pg->rank, pg->world_size, count, dt, uniform, im->rings, NULL, 0);
-  if (n < 0) { pg_set_error("plan: bad arguments"); return -1; }
+  if (n < 0) { pg_set_error("plan: bad arguments, or chunk_bytes too small for this count"); return -1; }
   if (n > im->steps_cap) {
     struct pg_step *s = (struct pg_step *)realloc(im->steps, sizeof(*s) * (size_t)n);
     if (!s) { pg_set_error("plan: out of host memory"); return -1; }

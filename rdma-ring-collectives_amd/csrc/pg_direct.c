@@ -69,7 +69,7 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
   if (pg_ensure(&im->ebuf, &im->ebuf_cap, (size_t)W * full * es)) return -1;
   char *gat = (char *)im->ebuf;                      /* STAGE0: slot q = rank q's copy of block r */
   int n = pg_plan_direct_reduce_scatter(r, W, count, dt, pg->chunk_bytes, pg->inflight, im->rings, NULL, 0);
-  if (n < 0) { pg_set_error("direct: bad plan arguments"); return -1; }
+  if (n < 0) { pg_set_error("direct: bad plan arguments, or chunk_bytes too small for this count"); return -1; }
   if (n > im->steps_cap) {
     struct pg_step *st = (struct pg_step *)realloc(im->steps, sizeof(*st) * (size_t)n);
     if (!st) { pg_set_error("direct: out of host memory"); return -1; }

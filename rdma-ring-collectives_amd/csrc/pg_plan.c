@@ -31,6 +31,8 @@
 #include "pg.h"
 #include "pg_ext.h"
 
+#define PG_MAX_PLAN_STEPS (1 << 28)
+
 static size_t plan_elem_size(int dt) {
   return dt == DT_INT32 ? 4 : dt == DT_DOUBLE ? 8 : 0;
 }
@@ -118,7 +120,12 @@ int pg_plan_reduce_scatter(int rank, int world, int count, int datatype,
   size_t bfull = ((size_t)count + (size_t)world - 1) / (size_t)world;
   size_t bh, bhl;
   pg_block_part(bfull, rings, 0, &bh, &bhl);         /* part 0 of a full block: the largest part */
-  int seg_stride = (int)nsegs(bhl, seg_elems_for(bhl, es, chunk_bytes, eager_max));
+  const size_t segs = nsegs(bhl, seg_elems_for(bhl, es, chunk_bytes, eager_max));
+  /* a plan is at most (world-1) rounds x rings x segs steps: refuse segment
+   * sizes so small that the step count (an int, like the event slots) would
+   * not fit -- the caller raises chunk_bytes */
+  if (segs > (size_t)PG_MAX_PLAN_STEPS / ((size_t)world * (size_t)rings)) return -1;
+  int seg_stride = (int)segs;
   int n = 0, batch = -1;
   for (int k = 0; k + 1 < world; ++k) {
     const int last = (k == world - 2);
@@ -255,8 +262,12 @@ int pg_plan_direct_reduce_scatter(int rank, int world, int count, int datatype, 
   const size_t full = ((size_t)count + (size_t)world - 1) / (size_t)world;
   size_t boff, blen;
   pg_block_range(count, world, rank, &boff, &blen);
+  const size_t seg = chunk_bytes / es ? chunk_bytes / es : 1;
+  /* at most ceil(full/seg) + rings segments, each a transfer step per peer
+   * plus a fold: refuse what would overflow the int step count */
+  if (full / seg + (size_t)rings > (size_t)PG_MAX_PLAN_STEPS / ((size_t)world + 1)) return -1;
   struct dseg d;
-  dseg_init(&d, full, rings, chunk_bytes / es);
+  dseg_init(&d, full, rings, seg);
   int n = 0, batch = 0;
   for (int s0 = 0; s0 < d.total; s0 += inflight, ++batch) {
     const int s1 = s0 + inflight < d.total ? s0 + inflight : d.total;

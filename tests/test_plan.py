@@ -218,3 +218,13 @@ def test_direct_plan_shape():
                 if s["recv_bytes"]:
                     assert s["recv_buf"] == pgamd.PG_BUF_STAGE0
                     assert q * 250 * es <= s["recv_off"] < (q + 1) * 250 * es
+
+
+def test_plans_refuse_absurd_step_counts(lib):
+    """A 4-byte segment over 2^30 elements would need billions of steps (an
+    int); both planners refuse it instead of overflowing, and the collective
+    reports it as a plan error."""
+    assert lib.pg_plan_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4, 0, 1, 2, 0, None, 0) == -1
+    assert lib.pg_plan_direct_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4, 1, 2, None, 0) == -1
+    assert lib.pg_plan_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4 << 20, 0, 4, 2, 0, None, 0) > 0
+    assert lib.pg_plan_direct_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4 << 20, 4, 2, None, 0) > 0
