@@ -1,7 +1,8 @@
 """BASELINE configs 3 and 4 at their full sizes through the real ring executor
-(W virtual ranks on the one test GPU: PG_TRANSPORT_THREADS keeps the plan,
-executor, streams, events, staging and the gfx950 kernel of the RCCL path and
-replaces only the hop by a device copy).
+and the direct exchange (PG_ALGO=direct, the rccl transport's default on one
+node) -- W virtual ranks on the one test GPU: PG_TRANSPORT_THREADS keeps the
+plan, executor, streams, events, staging and the gfx950 kernels of the RCCL
+path and replaces only the hop by a device copy.
 
 At these sizes the C oracle would need minutes, so the expected blocks are
 computed on the GPU with torch from the same inputs, in the fold order the
@@ -41,12 +42,15 @@ def _expected_block(torch, xs, b, off, ln, rings, world, op, oracle):
     return out
 
 
-@pytest.mark.parametrize("world,dt,count,rings", [
-    (4, pgamd.DT_INT32, 1 << 28, 2),        # config 3
-    (8, pgamd.DT_DOUBLE, 1 << 29, 2),       # config 4
-    (8, pgamd.DT_DOUBLE, 1 << 29, 4),       # config 4 over four rings
+@pytest.mark.parametrize("world,dt,count,rings,algo", [
+    (4, pgamd.DT_INT32, 1 << 28, 2, "ring"),        # config 3
+    (8, pgamd.DT_DOUBLE, 1 << 29, 2, "ring"),       # config 4
+    (8, pgamd.DT_DOUBLE, 1 << 29, 4, "ring"),       # config 4 over four rings
+    (4, pgamd.DT_INT32, 1 << 28, 2, "direct"),      # config 3, direct exchange
+    (8, pgamd.DT_DOUBLE, 1 << 29, 2, "direct"),     # config 4, direct exchange
 ])
-def test_baseline_config_full_size(gpu, lib, oracle, world, dt, count, rings):
+def test_baseline_config_full_size(gpu, lib, oracle, monkeypatch, world, dt, count, rings, algo):
+    monkeypatch.setenv("PG_ALGO", algo)
     torch = gpu
     g = torch.Generator(device="cuda").manual_seed(31 * world + rings)
     if dt == pgamd.DT_INT32:
@@ -76,10 +80,13 @@ def test_baseline_config_full_size(gpu, lib, oracle, world, dt, count, rings):
     torch.cuda.empty_cache()
 
 
-def test_baseline_config5_sequence(gpu, lib, oracle):
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_baseline_config5_sequence(gpu, lib, oracle, monkeypatch, algo):
     """config 5: 8 ranks, int32 and double products, eager-size calls (4 KiB)
     interleaved with 2 GiB calls on one set of handles (pgx_sim_run opens
-    fresh ones per call; the eager one-shot path and the ring both run)."""
+    fresh ones per call; the eager one-shot path and the ring or the direct
+    exchange both run)."""
+    monkeypatch.setenv("PG_ALGO", algo)
     torch = gpu
     world = 8
     g = torch.Generator(device="cuda").manual_seed(55)
@@ -111,10 +118,13 @@ def test_baseline_config5_sequence(gpu, lib, oracle):
             torch.cuda.empty_cache()
 
 
-def test_maximum_count_ring(gpu, lib, oracle):
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_maximum_count_ring(gpu, lib, oracle, monkeypatch, algo):
     """The API's largest count (INT_MAX int32 elements, 8 GiB per rank) through
-    the 2-rank ring: every byte offset of the plan and executor past 2^31 and
-    2^32, the ragged second block (one element shorter), both rings."""
+    the 2-rank ring and the direct exchange: every byte offset of the plan and
+    executor past 2^31 and 2^32, the ragged second block (one element
+    shorter), both rings."""
+    monkeypatch.setenv("PG_ALGO", algo)
     torch = gpu
     world, count = 2, (1 << 31) - 1
     g = torch.Generator(device="cuda").manual_seed(77)
