@@ -1,8 +1,10 @@
 /*
  * pg_xport_threads.c -- W virtual ranks inside one process, one GPU.
  *
- * RCCL refuses two ranks on one device, so a 1-GPU machine cannot run the real
- * ring with W > 1.  This transport keeps everything of the real path -- plan,
+ * RCCL refuses two ranks on one device unless each rank claims its own host
+ * (NCCL_HOSTID, tests/test_rccl_gpu.py), and then its hops ride sockets.  This
+ * transport runs up to 64 ranks in ONE process instead: it keeps everything of
+ * the real path -- plan,
  * executor, streams, events, staging, the gfx950 reduce kernel, the public
  * pg_* entry points -- and replaces only the hop: a send is published in a
  * per-edge FIFO and the receiving rank copies it device-to-device on its own
