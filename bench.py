@@ -266,6 +266,15 @@ def size_leg(lib, rank, world, reps=20):
             rows.append(["f64" if dt == pgamd.DT_DOUBLE else "i32", "sum" if op == pgamd.OP_SUM else "prod",
                          size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4),
                          round(sms * 1e3, 2), round(sgbs / HBM_PEAK_GBS, 4)])
+    # the per-launch edge: least-squares t = t0 + traffic / bw over the f64-sum rows >= 16 MiB
+    # (a fixed ramp + drain per launch against a streaming rate)
+    fit = {}
+    for col, key in ((3, "events"), (6, "stamped")):
+        pts = [(3 * r_[2], r_[col]) for r_ in rows if r_[0] == "f64" and r_[1] == "sum" and r_[2] >= (16 << 20)]
+        if len(pts) >= 3:
+            xs_, ys_ = np.array([p_[0] for p_ in pts], dtype=np.float64), np.array([p_[1] for p_ in pts])
+            slope, t0 = np.polyfit(xs_, ys_, 1)
+            fit[key] = {"t0_us": round(float(t0), 2), "stream_GBps": round(float(1.0 / slope / 1e3), 1)}
     batches = ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     direct = direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     lib.pgk_event_destroy(stamp[0])
@@ -273,7 +282,8 @@ def size_leg(lib, rank, world, reps=20):
     del pool
     torch.cuda.empty_cache()
     return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
-                        "stamped_frac"], "rows": rows, "ring_batches": batches, "direct_batches": direct,
+                        "stamped_frac"], "rows": rows, "edge_fit": fit, "ring_batches": batches,
+            "direct_batches": direct,
             "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
                       "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
                       "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
