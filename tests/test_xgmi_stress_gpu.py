@@ -1,4 +1,4 @@
-"""PG_TRANSPORT=xgmi under a long random sequence of collectives in one process
+"""PG_TRANSPORT=xgmi (and rccl, below) under a long random sequence of collectives in one process
 lifetime per rank: reduce-scatter / all-gather / all-reduce, int32 / double,
 sum / prod, sizes from 0 to 8 MiB, device / host / mixed buffers, in place,
 inputs that stay allocated across calls, fresh ones, and fresh allocations
@@ -46,10 +46,14 @@ def _sequence(seed, world):
     return seq
 
 
-def _worker(rank, world, port, q, mode, seed, rings):
-    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE=mode,
-                      PG_RINGS=str(rings))
+def _worker(rank, world, port, q, mode, seed, rings, transport="xgmi"):
+    os.environ.update(PG_TRANSPORT=transport, PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_RINGS=str(rings))
+    if transport == "xgmi":
+        os.environ["PG_XGMI_MODE"] = mode
+    else:        # the RCCL transport on one GPU: one host id per rank, hops over RCCL's socket transport
+        os.environ.update(PG_ALGO=mode, NCCL_HOSTID=f"pg-stress-{port}-rank{rank}", NCCL_SOCKET_IFNAME="lo",
+                          NCCL_IB_DISABLE="1")
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -120,7 +124,7 @@ def _worker(rank, world, port, q, mode, seed, rings):
             if got[:want.size].tobytes() != want.tobytes():
                 fails.append((i, coll, dt, op, count, mem, in_place, keep, flush))
         lib.pg_close(h)
-        if mode == "read" and zc == 0:
+        if transport == "xgmi" and mode == "read" and zc == 0:
             fails.append("no call read its inputs in place: zero-copy never exercised")
     except Exception as e:  # report, never hang the parent
         fails.append(("exception", repr(e)))
@@ -135,6 +139,33 @@ def test_xgmi_random_sequence(gpu, world, mode, seed, rings):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, seed, rings)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=420))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world,algo,seed,rings", [(3, "direct", 11, 2), (4, "ring", 12, 2), (2, "direct", 13, 1),
+                                                   (4, "direct", 14, 4)])
+def test_rccl_random_sequence(gpu, world, algo, seed, rings):
+    """The same random sequence over the RCCL transport (ring and direct
+    schedules; eager sizes, host / device / mixed buffers, in place, recycled
+    allocations), every call against the oracle ring."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, algo, seed, rings, "rccl")) for r in range(world)]
     for p in procs:
         p.start()
     results = []
