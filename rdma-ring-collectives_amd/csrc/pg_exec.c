@@ -85,6 +85,7 @@ int pg_kt_pair(struct pg_impl *im, void **t0, void **t1) {
     for (int i = im->n_kt_ev; i < cap; ++i) {
       hipError_t e = hipEventCreate(&im->kt_ev[i]);
       if (e != hipSuccess) {
+        if (i & 1) hipEventDestroy(im->kt_ev[i - 1]);     /* keep whole pairs */
         im->n_kt_ev = i & ~1;
         pg_set_error("pg_exec: hipEventCreate: %s", hipGetErrorString(e));
         return -1;

@@ -8,7 +8,8 @@ sizes, t = t0 + traffic / bw, splits the launch into a fixed edge t0 and a
 streaming rate bw (traffic: reduce/copy 3 or 2 bytes per operand byte, read 2,
 write 1).  The shipped pgk_reduce is timed the same way beside them.
 
-    python tools/lab/run_edge_lab.py [sizes in MiB ...]     (default 8 16 32 64 128 256)
+    python tools/lab/run_edge_lab.py [--lab edge|policy] [--b2b] [--reduce-only] [sizes in MiB ...]
+                                                            (default 8 16 32 64 128 256)
 """
 import ctypes
 import pathlib
@@ -25,10 +26,15 @@ import torch  # noqa: E402
 
 import pgamd  # noqa: E402
 
-so = HERE / "libedgelab.so"
+LAB = "edge"                    # --lab policy: tools/lab/policy_lab.hip (store cache policies), same API
+if "--lab" in sys.argv:
+    i = sys.argv.index("--lab")
+    LAB = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
+so = HERE / f"lib{LAB}lab.so"
 if not so.exists():
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
-                    str(HERE / "edge_lab.hip"), "-o", str(so)], check=True)
+                    str(HERE / f"{LAB}_lab.hip"), "-o", str(so)], check=True)
 lab = ctypes.CDLL(str(so))
 lab.edge_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                             ctypes.c_void_p, ctypes.c_void_p]
