@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""EXPERIMENTS ONLY: where one reduce launch's time goes, from per-workgroup
+timestamps (tools/lab/timeline_lab.hip, s_memrealtime at 100 MHz).
+
+For each operand size and tile shape, over a 4 GiB pool (HBM-resident), the
+diagnostic build is launched kernel-stamped (hipExtLaunchKernelGGL events, the
+figure rocprofv3 reports) and every block's entry / loads-returned /
+stores-acknowledged times are read back.  Per launch:
+
+  stamped     begin->end event time of the launch
+  span        first block entry -> last block's stores acknowledged
+  outside     stamped - span: dispatch of the first wave + end-of-kernel
+              completion (nothing of the kernel runs)
+  dispatch    first -> last block entry of the first resident round
+              (blocks that start before any block has finished)
+  first_load  first block: entry -> its loads returned (one loaded HBM round trip)
+  steady      bytes / time slope of block completions between 20% and 80%
+  head        time before completions follow the steady line (ramp)
+  tail        last completion minus the steady line's end (drain, incl. XCD imbalance)
+  xcd_end     spread of the 8 XCDs' last completions
+
+The shipped pgk_reduce is stamped beside it at the same size, so the build's
+perturbation (its waits) is visible; the shares, not the diagnostic's length,
+are the result.
+
+    python tools/lab/run_timeline_lab.py [sizes in MiB ...]      (default 16 64 256)
+"""
+import ctypes
+import pathlib
+import statistics
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+import torch  # noqa: E402
+
+import pgamd  # noqa: E402
+
+so = HERE / "libtimelinelab.so"
+if not so.exists():
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                    str(HERE / "timeline_lab.hip"), "-o", str(so)], check=True)
+lab = ctypes.CDLL(str(so))
+VP = ctypes.c_void_p
+lab.tl_launch.argtypes = [ctypes.c_int, VP, VP, ctypes.c_size_t, VP, VP, VP, VP]
+lab.tl_grid.argtypes = [ctypes.c_int, ctypes.c_size_t]
+lab.tl_grid.restype = ctypes.c_uint
+lib = pgamd.load()
+torch.cuda.set_device(0)
+sh = torch.cuda.current_stream().cuda_stream
+khz = ctypes.c_int()
+assert lab.tl_clock_khz(ctypes.byref(khz)) == 0
+TICK_US = 1e3 / khz.value                       # 100 MHz -> 0.01 us
+POOL = 4 << 30
+pool = torch.empty(POOL // 8, dtype=torch.float64, device="cuda").uniform_(-1, 1)
+base = pool.data_ptr()
+ev = (VP(), VP())
+pgamd.check(lib.pgk_event_create(ctypes.byref(ev[0])), "event")
+pgamd.check(lib.pgk_event_create(ctypes.byref(ev[1])), "event")
+SHAPES = {0: "512x2", 1: "1024x1"}
+REPS = 8
+
+
+def elapsed_us():
+    ms = ctypes.c_float()
+    pgamd.check(lib.pgk_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)), "elapsed")
+    return ms.value * 1e3
+
+
+def analyse(ts, tile_bytes, stamped):
+    ent, ld, st, xcc = (ts[:, 0].astype(np.int64), ts[:, 1].astype(np.int64), ts[:, 2].astype(np.int64),
+                        ts[:, 3].astype(np.int64))
+    t0 = ent.min()
+    ent, ld, st = (ent - t0) * TICK_US, (ld - t0) * TICK_US, (st - t0) * TICK_US
+    span = st.max()
+    first_done = st.min()
+    first_round = ent < first_done
+    order = np.argsort(st)
+    done = st[order]
+    cum = np.arange(1, len(done) + 1) * 3.0 * tile_bytes
+    lo, hi = int(0.2 * len(done)), int(0.8 * len(done))
+    k, a = np.polyfit(cum[lo:hi], done[lo:hi], 1)          # t = a + k * bytes
+    total = cum[-1]
+    first_blk = np.argmin(ent)
+    xcd_last = [st[xcc == x].max() for x in np.unique(xcc)]
+    return {"stamped": stamped, "span": span, "outside": stamped - span,
+            "resident": int(first_round.sum()), "dispatch": ent[first_round].max(),
+            "first_load": ld[first_blk] - ent[first_blk],
+            "load_med": float(np.median(ld - ent)), "store_med": float(np.median(st - ld)),
+            "steady_gbs": 1.0 / k / 1e3, "head": a, "tail": span - (a + k * total),
+            "xcd_end": max(xcd_last) - min(xcd_last), "n_xcc": len(xcd_last)}
+
+
+sizes = [int(a) << 20 for a in sys.argv[1:]] or [m << 20 for m in (16, 64, 256)]
+k = 0
+for size in sizes:
+    n = size // 8
+    pairs = POOL // (2 * size)
+    for shape, sname in SHAPES.items():
+        grid = lab.tl_grid(shape, n)
+        ts_dev = torch.zeros(4 * grid, dtype=torch.int64, device="cuda")
+        rows, shipped = [], []
+        for rep in range(REPS + 1):
+            d = base + 2 * size * (k % pairs)
+            k += 1
+            assert lab.tl_launch(shape, d, d + size, n, ts_dev.data_ptr(), sh, ev[0], ev[1]) == 0
+            torch.cuda.synchronize()
+            st_us = elapsed_us()
+            ts = ts_dev.view(grid, 4).cpu().numpy()
+            d = base + 2 * size * (k % pairs)
+            k += 1
+            pgamd.check(lib.pgk_reduce_timed(d, d + size, n, 1, 0, sh, ev[0], ev[1]), "shipped")
+            torch.cuda.synchronize()
+            if rep:                                   # the first of each is a warm-up
+                rows.append(analyse(ts, 1024 * 16, st_us))
+                shipped.append(elapsed_us())
+        med = {key: statistics.median(r[key] for r in rows) for key in rows[0]}
+        print(f"== {size >> 20} MiB per operand, {sname} tiles, {grid} blocks (medians of {REPS} launches, us) ==")
+        print(f"  shipped pgk_reduce stamped {statistics.median(shipped):8.2f}   diagnostic build stamped "
+              f"{med['stamped']:8.2f}")
+        print(f"  span {med['span']:8.2f}  outside {med['outside']:6.2f}  | resident first round {med['resident']:.0f} "
+              f"blocks, dispatched over {med['dispatch']:5.2f}")
+        print(f"  first block loads {med['first_load']:5.2f}  median block: loads {med['load_med']:5.2f}, "
+              f"stores acked {med['store_med']:5.2f}")
+        print(f"  steady {med['steady_gbs']:7.1f} GB/s  head {med['head']:5.2f}  tail {med['tail']:5.2f}  "
+              f"XCD last-completion spread {med['xcd_end']:5.2f} over {med['n_xcc']:.0f} XCDs", flush=True)
+        del ts_dev
