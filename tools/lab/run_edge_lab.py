@@ -8,7 +8,7 @@ sizes, t = t0 + traffic / bw, splits the launch into a fixed edge t0 and a
 streaming rate bw (traffic: reduce/copy 3 or 2 bytes per operand byte, read 2,
 write 1).  The shipped pgk_reduce is timed the same way beside them.
 
-    python tools/lab/run_edge_lab.py [--lab edge|policy] [--b2b] [--reduce-only] [sizes in MiB ...]
+    python tools/lab/run_edge_lab.py [--lab edge|policy|wait|dyn] [--only TEXT] [--b2b] [--reduce-only] [sizes in MiB ...]
                                                             (default 8 16 32 64 128 256)
 """
 import ctypes
@@ -54,6 +54,11 @@ variants = [-1] + [v for v in range(32) if lab.edge_name(v)]
 B2B = "--b2b" in sys.argv       # events bracketing back-to-back launches (the bench's kernel_us) instead of stamps
 if B2B:
     sys.argv.remove("--b2b")
+if "--only" in sys.argv:                       # variants whose name contains this text (and the shipped kernel)
+    i = sys.argv.index("--only")
+    only = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
+    variants = [v for v in variants if v < 0 or only in lab.edge_name(v).decode()]
 if "--reduce-only" in sys.argv:
     sys.argv.remove("--reduce-only")
     variants = [v for v in variants if v < 0 or lab.edge_name(v).decode().startswith("reduce")]

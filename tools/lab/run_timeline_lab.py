@@ -87,7 +87,10 @@ def analyse(ts, tile_bytes, stamped):
     total = cum[-1]
     first_blk = np.argmin(ent)
     xcd_last = [st[xcc == x].max() for x in np.unique(xcc)]
-    return {"stamped": stamped, "span": span, "outside": stamped - span,
+    per_xcd = {int(x): (int((xcc == x).sum()), span - st[xcc == x].max(),
+                        3.0 * tile_bytes * (xcc == x).sum() / (st[xcc == x].max() - ent[xcc == x].min()) / 1e3)
+               for x in np.unique(xcc)}
+    return {"per_xcd": per_xcd, "stamped": stamped, "span": span, "outside": stamped - span,
             "resident": int(first_round.sum()), "dispatch": ent[first_round].max(),
             "first_load": ld[first_blk] - ent[first_blk],
             "load_med": float(np.median(ld - ent)), "store_med": float(np.median(st - ld)),
@@ -118,6 +121,7 @@ for size in sizes:
             if rep:                                   # the first of each is a warm-up
                 rows.append(analyse(ts, 1024 * 16, st_us))
                 shipped.append(elapsed_us())
+        per = [r.pop("per_xcd") for r in rows]
         med = {key: statistics.median(r[key] for r in rows) for key in rows[0]}
         print(f"== {size >> 20} MiB per operand, {sname} tiles, {grid} blocks (medians of {REPS} launches, us) ==")
         print(f"  shipped pgk_reduce stamped {statistics.median(shipped):8.2f}   diagnostic build stamped "
@@ -128,4 +132,13 @@ for size in sizes:
               f"stores acked {med['store_med']:5.2f}")
         print(f"  steady {med['steady_gbs']:7.1f} GB/s  head {med['head']:5.2f}  tail {med['tail']:5.2f}  "
               f"XCD last-completion spread {med['xcd_end']:5.2f} over {med['n_xcc']:.0f} XCDs", flush=True)
+        # per XCD (HW_REG_XCC_ID): blocks, how long before the launch's last completion it finished
+        # (median over launches; and in each launch), and its own rate over its span
+        ids = sorted(set().union(*[set(p) for p in per]))
+        print("  per XCD: id blocks | finished early by (median; each launch) | GB/s over its own span")
+        for x in ids:
+            early = [p[x][1] for p in per if x in p]
+            rate = [p[x][2] for p in per if x in p]
+            print(f"    {x}  {per[0].get(x, (0,))[0]:6d} | {statistics.median(early):5.2f}; "
+                  + " ".join(f"{e:4.1f}" for e in early) + f" | {statistics.median(rate):7.1f}")
         del ts_dev
