@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""EXPERIMENTS ONLY: results of tools/lab/dyn_lab.hip's variants against torch
-(dst + src), at ragged and full sizes, and its counters back at zero after
-every launch.  Prints one line per variant and size; exits 1 on a mismatch."""
+"""EXPERIMENTS ONLY: results of tools/lab/dyn_lab.hip's (or, with --lab wgt,
+wgt_lab.hip's) variants against torch (dst + src), at ragged and full sizes,
+and the ticket counters back at zero after every launch.  Prints one line per
+variant and size; exits 1 on a mismatch.
+
+    python tools/lab/check_dyn_lab.py [--lab dyn|wgt] [name filter]"""
 import ctypes
 import pathlib
 import sys
@@ -9,7 +12,12 @@ import sys
 import torch
 
 HERE = pathlib.Path(__file__).resolve().parent
-lab = ctypes.CDLL(str(HERE / "libdynlab.so"))
+LAB = "dyn"
+if "--lab" in sys.argv:
+    i = sys.argv.index("--lab")
+    LAB = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
+lab = ctypes.CDLL(str(HERE / f"lib{LAB}lab.so"))
 lab.edge_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                             ctypes.c_void_p, ctypes.c_void_p]
 lab.edge_name.restype = ctypes.c_char_p
@@ -24,7 +32,7 @@ for v in range(64):
     name = name.decode()
     if only not in name:
         continue
-    for n in (2, 2048, 1 << 20, (1 << 20) + 2 * 777, 3 * (1 << 22) + 2 * 5, 1 << 25):
+    for n in (2, 2048, 4094, 4096 + 2 * 17, 1 << 20, (1 << 20) + 2 * 777, 3 * (1 << 22) + 2 * 5, 1 << 25):
         x = torch.rand(n, dtype=torch.float64, device="cuda")
         y = torch.rand(n, dtype=torch.float64, device="cuda")
         ref = x + y

@@ -61,7 +61,7 @@ base = pool.data_ptr()
 ev = (VP(), VP())
 pgamd.check(lib.pgk_event_create(ctypes.byref(ev[0])), "event")
 pgamd.check(lib.pgk_event_create(ctypes.byref(ev[1])), "event")
-SHAPES = {0: "512x2", 1: "1024x1"}
+SHAPES = {0: "512x2", 1: "1024x1", 2: "512x2 swapped", 3: "1024x1 swapped"}
 REPS = 8
 
 
@@ -90,7 +90,9 @@ def analyse(ts, tile_bytes, stamped):
     per_xcd = {int(x): (int((xcc == x).sum()), span - st[xcc == x].max(),
                         3.0 * tile_bytes * (xcc == x).sum() / (st[xcc == x].max() - ent[xcc == x].min()) / 1e3)
                for x in np.unique(xcc)}
-    return {"per_xcd": per_xcd, "stamped": stamped, "span": span, "outside": stamped - span,
+    # block b -> XCD (b + c) mod 8 under strict round-robin dealing: the set of c over the launch
+    cset = sorted(set(((xcc - np.arange(len(xcc))) % 8).tolist()))
+    return {"cset": cset, "per_xcd": per_xcd, "stamped": stamped, "span": span, "outside": stamped - span,
             "resident": int(first_round.sum()), "dispatch": ent[first_round].max(),
             "first_load": ld[first_blk] - ent[first_blk],
             "load_med": float(np.median(ld - ent)), "store_med": float(np.median(st - ld)),
@@ -98,6 +100,12 @@ def analyse(ts, tile_bytes, stamped):
             "xcd_end": max(xcd_last) - min(xcd_last), "n_xcc": len(xcd_last)}
 
 
+if "--swap-only" in sys.argv:        # only the parity-swapped shapes (and 512x2 for reference)
+    sys.argv.remove("--swap-only")
+    SHAPES = {0: "512x2", 2: "512x2 swapped", 3: "1024x1 swapped"}
+PRE_ODD = "--pre-odd" in sys.argv    # a 3-block pgk_reduce launch before each stamped one: does dealing continue?
+if PRE_ODD:
+    sys.argv.remove("--pre-odd")
 sizes = [int(a) << 20 for a in sys.argv[1:]] or [m << 20 for m in (16, 64, 256)]
 k = 0
 for size in sizes:
@@ -110,6 +118,8 @@ for size in sizes:
         for rep in range(REPS + 1):
             d = base + 2 * size * (k % pairs)
             k += 1
+            if PRE_ODD:
+                pgamd.check(lib.pgk_reduce(base, base + (8 << 20), 3 * 2048, 1, 0, sh), "pre")
             assert lab.tl_launch(shape, d, d + size, n, ts_dev.data_ptr(), sh, ev[0], ev[1]) == 0
             torch.cuda.synchronize()
             st_us = elapsed_us()
@@ -122,6 +132,7 @@ for size in sizes:
                 rows.append(analyse(ts, 1024 * 16, st_us))
                 shipped.append(elapsed_us())
         per = [r.pop("per_xcd") for r in rows]
+        csets = [r.pop("cset") for r in rows]
         med = {key: statistics.median(r[key] for r in rows) for key in rows[0]}
         print(f"== {size >> 20} MiB per operand, {sname} tiles, {grid} blocks (medians of {REPS} launches, us) ==")
         print(f"  shipped pgk_reduce stamped {statistics.median(shipped):8.2f}   diagnostic build stamped "
@@ -134,6 +145,7 @@ for size in sizes:
               f"XCD last-completion spread {med['xcd_end']:5.2f} over {med['n_xcc']:.0f} XCDs", flush=True)
         # per XCD (HW_REG_XCC_ID): blocks, how long before the launch's last completion it finished
         # (median over launches; and in each launch), and its own rate over its span
+        print(f"  dealing: c in xcc = (b + c) mod 8, per launch: {csets}")
         ids = sorted(set().union(*[set(p) for p in per]))
         print("  per XCD: id blocks | finished early by (median; each launch) | GB/s over its own span")
         for x in ids:

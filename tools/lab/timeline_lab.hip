@@ -27,12 +27,15 @@ __device__ __forceinline__ unsigned xcc_id() {
   return v & 0xf;
 }
 
-template <int B, int U>
+// SWAP: block b takes tile b ^ ((b >> 3) & 1), so the XCD of block b (b mod 8)
+// works on tiles of both parities (address bit 14 at 16 KiB tiles) in turn
+template <int B, int U, bool SWAP>
 __global__ __launch_bounds__(B) void k_reduce_tl(f64x2* __restrict__ d, const f64x2* __restrict__ s, size_t nvec,
                                                  unsigned long long* __restrict__ ts) {
   const unsigned long long t_entry = stamp();
-  const size_t i = (size_t)blockIdx.x * B * U + threadIdx.x;
-  const bool full = (size_t)(blockIdx.x + 1) * B * U <= nvec;   // every block but a ragged last one
+  const size_t t = SWAP ? (blockIdx.x ^ ((blockIdx.x >> 3) & 1)) : blockIdx.x;
+  const size_t i = t * B * U + threadIdx.x;
+  const bool full = (t + 1) * B * U <= nvec;   // every tile but a ragged last one
   f64x2 x[U], y[U];
   if (full) {
 #pragma unroll
@@ -74,10 +77,10 @@ extern "C" int tl_clock_khz(int* khz) {
   return hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, 0) == hipSuccess ? 0 : -1;
 }
 
-// shape 0: 512x2 (shipped below 128 MiB per operand), 1: 1024x1 (shipped from 256 MiB)
+// shape 0: 512x2 (shipped below 128 MiB per operand), 1: 1024x1 (shipped from 256 MiB); 2, 3: the same, SWAP
 extern "C" unsigned tl_grid(int shape, size_t n) {
-  (void)shape;                                  // 512 x 2 and 1024 x 1: 1024 vectors per block either way
-  return (unsigned)((n / 2 + 1023) / 1024);
+  const size_t tiles = (n / 2 + 1023) / 1024;   // 512 x 2 and 1024 x 1: 1024 vectors per block either way
+  return (unsigned)(shape >= 2 ? (tiles + 15) / 16 * 16 : tiles);   // swapped shapes permute within 16
 }
 
 extern "C" int tl_launch(int shape, double* d, const double* s, size_t n, unsigned long long* ts, void* stream,
@@ -88,10 +91,16 @@ extern "C" int tl_launch(int shape, double* d, const double* s, size_t n, unsign
   const size_t nvec = n / 2;
   const unsigned grid = tl_grid(shape, n);
   if (shape == 0)
-    hipExtLaunchKernelGGL((k_reduce_tl<512, 2>), dim3(grid), dim3(512), 0, st, a, b, 0, (f64x2*)d,
+    hipExtLaunchKernelGGL((k_reduce_tl<512, 2, false>), dim3(grid), dim3(512), 0, st, a, b, 0, (f64x2*)d,
                           (const f64x2*)s, nvec, ts);
   else if (shape == 1)
-    hipExtLaunchKernelGGL((k_reduce_tl<1024, 1>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
+    hipExtLaunchKernelGGL((k_reduce_tl<1024, 1, false>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
+                          (const f64x2*)s, nvec, ts);
+  else if (shape == 2)
+    hipExtLaunchKernelGGL((k_reduce_tl<512, 2, true>), dim3(grid), dim3(512), 0, st, a, b, 0, (f64x2*)d,
+                          (const f64x2*)s, nvec, ts);
+  else if (shape == 3)
+    hipExtLaunchKernelGGL((k_reduce_tl<1024, 1, true>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
                           (const f64x2*)s, nvec, ts);
   else
     return -1;
