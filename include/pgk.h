@@ -39,7 +39,9 @@ extern "C" {
  * IEEE-754 add or multiply per element (round-to-nearest, denormals kept), so
  * results are bit-identical to the reference loop for every non-NaN result.
  * dst and src must not partially overlap (dst == src is allowed).
- * n == 0 is a no-op returning 0.  dt/op outside the values above -> -1. */
+ * n == 0 is a no-op returning 0.  dt/op outside the values above -> -1.
+ * Above 512 MiB per operand the call is several back-to-back launches on
+ * `stream` (each at most 512 MiB), which measure faster than one. */
 PG_API int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *stream);
 
 /* out[i] = a[i] op b[i] (out may equal a or b).  Same numerics as pgk_reduce;
@@ -108,7 +110,9 @@ PG_API int pgk_event_create(void **event);
 PG_API int pgk_event_destroy(void *event);
 PG_API int pgk_event_elapsed_ms(void *start_event, void *stop_event, float *ms);
 
-/* Grid the next pgk_reduce of n elements of dt would launch (for bench/tests). */
+/* Grid the next pgk_reduce of n elements of dt would launch (for bench/tests).
+ * A call above 512 MiB per operand is cut into equal launches of at most
+ * 512 MiB (pgk_reduce.hip, kSplitBytes); this reports the first of them. */
 PG_API int pgk_launch_geometry(size_t n, int dt, unsigned *grid, unsigned *block);
 
 /* Last error message of the calling thread ("" if none). */

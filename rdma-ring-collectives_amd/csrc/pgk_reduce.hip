@@ -392,16 +392,50 @@ void launch_vec(const Plan& p, T* out, const T* a, const T* b, hipStream_t s, Ti
   }
 }
 
+// A single vector launch over more than 512 MiB per operand streams 1.3-4%
+// slower than the same operands cut into launches of at most 512 MiB, on two
+// boxes, at 1 and 2 GiB per operand, in every tile shape; the block count is
+// not the cause (a 32 KiB tile halves it and is slower still;
+// tools/lab/split_probe.py, profiles/r02_split_probe.txt).  So the size-chosen
+// path cuts such a call into ceil(bytes / 512 MiB) equal pieces, each a whole
+// number of 16 KiB tiles (every piece keeps the operands' 16-B phase), launched
+// back to back on the caller's stream; the start stamp goes on the first, the
+// stop stamp on the last.  A shape forced by pgk_tune_shape stays one launch,
+// as the labs measure it.  The element-wise path (misaligned operands) is not
+// cut: it is the rare fallback, and one launch keeps its grid-stride tested.
+constexpr size_t kSplitBytes = 512ull << 20;
+
+// elements per piece of an n-element vector call (n when it is not cut)
+size_t piece_elems(size_t n, size_t es) {
+  const size_t pieces = (n * es + kSplitBytes - 1) / kSplitBytes;
+  if (g_block || pieces < 2) return n;
+  const size_t align = (16u << 10) / es;
+  return ((n + pieces - 1) / pieces + align - 1) / align * align;
+}
+
 template <typename T, int OP>
 hipError_t launch_t(T* out, const T* a, const T* b, size_t n, hipStream_t s, Timing tm) {
   Plan p = plan_for(out, a, b, n, sizeof(T));
   if (p.vec) {
-    if (g_nontemporal) launch_vec<T, OP, true>(p, out, a, b, s, tm);
-    else launch_vec<T, OP, false>(p, out, a, b, s, tm);
-  } else {
-    hipExtLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(p.grid), dim3(kScalarBlock), 0, s, tm.start, tm.stop, 0,
-                          out, a, b, n);
+    const size_t piece = piece_elems(n, sizeof(T));
+    if (piece >= n) {
+      if (g_nontemporal) launch_vec<T, OP, true>(p, out, a, b, s, tm);
+      else launch_vec<T, OP, false>(p, out, a, b, s, tm);
+      return hipGetLastError();
+    }
+    for (size_t off = 0; off < n; off += piece) {
+      const size_t len = n - off < piece ? n - off : piece;
+      const Plan q = plan_for(out + off, a + off, b + off, len, sizeof(T));
+      const Timing tq{off == 0 ? tm.start : nullptr, off + len == n ? tm.stop : nullptr};
+      if (g_nontemporal) launch_vec<T, OP, true>(q, out + off, a + off, b + off, s, tq);
+      else launch_vec<T, OP, false>(q, out + off, a + off, b + off, s, tq);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
+  hipExtLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(p.grid), dim3(kScalarBlock), 0, s, tm.start, tm.stop, 0,
+                        out, a, b, n);
   return hipGetLastError();
 }
 
@@ -765,7 +799,8 @@ int pgk_event_elapsed_ms(void* start, void* stop, float* ms) {
 
 int pgk_launch_geometry(size_t n, int dt, unsigned* grid, unsigned* block) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
-  Plan p = plan_for(nullptr, nullptr, nullptr, n, dt == PGK_DT_INT32 ? 4 : 8);
+  const size_t es = dt == PGK_DT_INT32 ? 4 : 8;
+  Plan p = plan_for(nullptr, nullptr, nullptr, piece_elems(n, es), es);   // the first launch of the call
   if (grid) *grid = p.grid;
   if (block) *block = p.vec ? (unsigned)p.block : (unsigned)kScalarBlock;
   return 0;

@@ -72,6 +72,10 @@ def test_launch_geometry(lib):
     for n, dt in ((1 << 40, 1), (1 << 36, 0), ((1 << 31) - 1, 1), (1 << 33, 0)):
         assert lib.pgk_launch_geometry(n, dt, ctypes.byref(g), ctypes.byref(b)) == 0
         assert 1 <= g.value and g.value * b.value < 1 << 32, (n, dt, g.value, b.value)
+    # above 512 MiB per operand the call is cut into <= 512 MiB launches: the first one's grid
+    for n, dt, grid in ((1 << 26, 1, 32768), ((1 << 26) + 1, 1, 16385), (1 << 27, 1, 32768), (1 << 28, 0, 32768)):
+        assert lib.pgk_launch_geometry(n, dt, ctypes.byref(g), ctypes.byref(b)) == 0
+        assert (g.value, b.value) == (grid, 1024), (n, dt, g.value, b.value)
 
 
 def test_connect_without_gpu_fails_cleanly(lib):

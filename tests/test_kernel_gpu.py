@@ -141,6 +141,37 @@ def test_full_size_config2(gpu, lib, oracle):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("nbytes", [512 << 20, (512 << 20) + 8, (1 << 30) + 24])
+def test_split_launches(gpu, lib, oracle, nbytes):
+    """Above 512 MiB per operand pgk_reduce is several back-to-back launches of
+    at most 512 MiB (kSplitBytes in pgk_reduce.hip): exactly 512 MiB stays one
+    launch, 512 MiB + 8 B is two, 1 GiB + 24 B three.  Every element against the
+    oracle, the head element (one element past the 16-B phase) and the bytes
+    around the range untouched, and the stamped form brackets all the pieces."""
+    import ctypes
+    torch = gpu
+    for dt, op in ((1, 0), (0, 1)):
+        es = 4 if dt == 0 else 8
+        n = nbytes // es
+        a, b = oracle.fill(n + 2, dt, op, 61), oracle.fill(n + 2, dt, op, 62)
+        d, s = to_dev(torch, a), to_dev(torch, b)
+        e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.pgk_event_create(ctypes.byref(e0)) == 0 and lib.pgk_event_create(ctypes.byref(e1)) == 0
+        assert lib.pgk_reduce_timed(ptr(d) + es, ptr(s) + es, n, dt, op, stream(torch), e0, e1) == 0
+        torch.cuda.synchronize()
+        ms = ctypes.c_float()
+        assert lib.pgk_event_elapsed_ms(e0, e1, ctypes.byref(ms)) == 0
+        assert 3 * nbytes / (ms.value * 1e-3) < 8.0e12 * 1.05, ms.value     # the stamps bracket every piece
+        lib.pgk_event_destroy(e0)
+        lib.pgk_event_destroy(e1)
+        got = to_host(torch, d)
+        want = a.copy()
+        want[1:n + 1] = oracle.reduce(a[1:n + 1], b[1:n + 1], dt, op)
+        assert got.tobytes() == want.tobytes(), (dt, op, nbytes)
+        del d, s, got, want
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("nbytes", [(128 << 20) - 16, 128 << 20, (160 << 20) + 24, (256 << 20) - 8, 256 << 20])
 def test_default_shape_boundaries(gpu, lib, oracle, nbytes):
     """Each size-chosen vector shape (shape_for in pgk_reduce.hip: 512x2 below
