@@ -92,7 +92,18 @@ def analyse(ts, tile_bytes, stamped):
                for x in np.unique(xcc)}
     # block b -> XCD (b + c) mod 8 under strict round-robin dealing: the set of c over the launch
     cset = sorted(set(((xcc - np.arange(len(xcc))) % 8).tolist()))
-    return {"cset": cset, "per_xcd": per_xcd, "stamped": stamped, "span": span, "outside": stamped - span,
+    # streaming rate in each tenth of the span (completions' bytes / time): does it decay along a long launch?
+    edges = np.linspace(0, span, 11)
+    cnt = np.histogram(st, bins=edges)[0]
+    deciles = (cnt * 3.0 * tile_bytes / (span / 10) / 1e3).tolist()
+    # how far apart in the buffer are the tiles finishing together?  5-95% range of the block
+    # index (= tile index in the unswapped shapes) among the blocks completing in each tenth, in MiB
+    # per operand: XCDs streaming at different rates drift apart over a launch
+    which = np.digitize(st, edges[1:-1])
+    bidx = np.arange(len(st))
+    spread = [float(np.subtract(*np.percentile(bidx[which == k], [95, 5])) * tile_bytes / 2**20)
+              if (which == k).sum() > 8 else 0.0 for k in range(10)]
+    return {"cset": cset, "per_xcd": per_xcd, "deciles": deciles, "spread": spread, "stamped": stamped, "span": span, "outside": stamped - span,
             "resident": int(first_round.sum()), "dispatch": ent[first_round].max(),
             "first_load": ld[first_blk] - ent[first_blk],
             "load_med": float(np.median(ld - ent)), "store_med": float(np.median(st - ld)),
@@ -133,6 +144,8 @@ for size in sizes:
                 shipped.append(elapsed_us())
         per = [r.pop("per_xcd") for r in rows]
         csets = [r.pop("cset") for r in rows]
+        dec = np.median(np.array([r.pop("deciles") for r in rows]), axis=0)
+        spr = np.median(np.array([r.pop("spread") for r in rows]), axis=0)
         med = {key: statistics.median(r[key] for r in rows) for key in rows[0]}
         print(f"== {size >> 20} MiB per operand, {sname} tiles, {grid} blocks (medians of {REPS} launches, us) ==")
         print(f"  shipped pgk_reduce stamped {statistics.median(shipped):8.2f}   diagnostic build stamped "
@@ -145,6 +158,8 @@ for size in sizes:
               f"XCD last-completion spread {med['xcd_end']:5.2f} over {med['n_xcc']:.0f} XCDs", flush=True)
         # per XCD (HW_REG_XCC_ID): blocks, how long before the launch's last completion it finished
         # (median over launches; and in each launch), and its own rate over its span
+        print("  GB/s by tenth of the span: " + " ".join(f"{v:6.0f}" for v in dec))
+        print("  MiB apart (5-95%) of the tiles finishing in each tenth: " + " ".join(f"{v:6.1f}" for v in spr))
         print(f"  dealing: c in xcc = (b + c) mod 8, per launch: {csets}")
         ids = sorted(set().union(*[set(p) for p in per]))
         print("  per XCD: id blocks | finished early by (median; each launch) | GB/s over its own span")
