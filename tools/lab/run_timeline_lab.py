@@ -71,7 +71,7 @@ def elapsed_us():
     return ms.value * 1e3
 
 
-def analyse(ts, tile_bytes, stamped):
+def analyse(ts, tile_bytes, stamped, factor=3.0):
     ent, ld, st, xcc = (ts[:, 0].astype(np.int64), ts[:, 1].astype(np.int64), ts[:, 2].astype(np.int64),
                         ts[:, 3].astype(np.int64))
     t0 = ent.min()
@@ -81,21 +81,21 @@ def analyse(ts, tile_bytes, stamped):
     first_round = ent < first_done
     order = np.argsort(st)
     done = st[order]
-    cum = np.arange(1, len(done) + 1) * 3.0 * tile_bytes
+    cum = np.arange(1, len(done) + 1) * factor * tile_bytes
     lo, hi = int(0.2 * len(done)), int(0.8 * len(done))
     k, a = np.polyfit(cum[lo:hi], done[lo:hi], 1)          # t = a + k * bytes
     total = cum[-1]
     first_blk = np.argmin(ent)
     xcd_last = [st[xcc == x].max() for x in np.unique(xcc)]
     per_xcd = {int(x): (int((xcc == x).sum()), span - st[xcc == x].max(),
-                        3.0 * tile_bytes * (xcc == x).sum() / (st[xcc == x].max() - ent[xcc == x].min()) / 1e3)
+                        factor * tile_bytes * (xcc == x).sum() / (st[xcc == x].max() - ent[xcc == x].min()) / 1e3)
                for x in np.unique(xcc)}
     # block b -> XCD (b + c) mod 8 under strict round-robin dealing: the set of c over the launch
     cset = sorted(set(((xcc - np.arange(len(xcc))) % 8).tolist()))
     # streaming rate in each tenth of the span (completions' bytes / time): does it decay along a long launch?
     edges = np.linspace(0, span, 11)
     cnt = np.histogram(st, bins=edges)[0]
-    deciles = (cnt * 3.0 * tile_bytes / (span / 10) / 1e3).tolist()
+    deciles = (cnt * factor * tile_bytes / (span / 10) / 1e3).tolist()
     # how far apart in the buffer are the tiles finishing together?  5-95% range of the block
     # index (= tile index in the unswapped shapes) among the blocks completing in each tenth, in MiB
     # per operand: XCDs streaming at different rates drift apart over a launch
@@ -111,6 +111,10 @@ def analyse(ts, tile_bytes, stamped):
             "xcd_end": max(xcd_last) - min(xcd_last), "n_xcc": len(xcd_last)}
 
 
+STREAMS = "--streams" in sys.argv  # the 1024x1 reduce beside a loads-only and a stores-only build
+if STREAMS:
+    sys.argv.remove("--streams")
+    SHAPES = {1: "1024x1", 4: "1024x1 loads only", 5: "1024x1 stores only"}
 if "--swap-only" in sys.argv:        # only the parity-swapped shapes (and 512x2 for reference)
     sys.argv.remove("--swap-only")
     SHAPES = {0: "512x2", 2: "512x2 swapped", 3: "1024x1 swapped"}
@@ -140,7 +144,7 @@ for size in sizes:
             pgamd.check(lib.pgk_reduce_timed(d, d + size, n, 1, 0, sh, ev[0], ev[1]), "shipped")
             torch.cuda.synchronize()
             if rep:                                   # the first of each is a warm-up
-                rows.append(analyse(ts, 1024 * 16, st_us))
+                rows.append(analyse(ts, 1024 * 16, st_us, {4: 2.0, 5: 1.0}.get(shape, 3.0)))
                 shipped.append(elapsed_us())
         per = [r.pop("per_xcd") for r in rows]
         csets = [r.pop("cset") for r in rows]

@@ -28,8 +28,12 @@ __device__ __forceinline__ unsigned xcc_id() {
 }
 
 // SWAP: block b takes tile b ^ ((b >> 3) & 1), so the XCD of block b (b mod 8)
-// works on tiles of both parities (address bit 14 at 16 KiB tiles) in turn
-template <int B, int U, bool SWAP>
+// works on tiles of both parities (address bit 14 at 16 KiB tiles) in turn.
+// MODE 0: the reduce; 1: loads only (the sum is stored only if it is NaN,
+// which the runner's inputs never are); 2: stores only (dst = src's address
+// as a double, no loads).  Modes 1 and 2 ask which stream the rate decay
+// over a long launch belongs to.
+template <int B, int U, bool SWAP, int MODE = 0>
 __global__ __launch_bounds__(B) void k_reduce_tl(f64x2* __restrict__ d, const f64x2* __restrict__ s, size_t nvec,
                                                  unsigned long long* __restrict__ ts) {
   const unsigned long long t_entry = stamp();
@@ -37,7 +41,13 @@ __global__ __launch_bounds__(B) void k_reduce_tl(f64x2* __restrict__ d, const f6
   const size_t i = t * B * U + threadIdx.x;
   const bool full = (t + 1) * B * U <= nvec;   // every tile but a ragged last one
   f64x2 x[U], y[U];
-  if (full) {
+  if (MODE == 2) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = f64x2{(double)(i + u * B), 0.0};
+      y[u] = f64x2{0.0, 0.0};
+    }
+  } else if (full) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       x[u] = __builtin_nontemporal_load(d + i + u * B);
@@ -53,7 +63,13 @@ __global__ __launch_bounds__(B) void k_reduce_tl(f64x2* __restrict__ d, const f6
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t_loaded = stamp();
-  if (full) {
+  if (MODE == 1) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f64x2 v = x[u] + y[u];
+      if (i + u * B < nvec && (v.x != v.x)) __builtin_nontemporal_store(v, d + i + u * B);
+    }
+  } else if (full) {
 #pragma unroll
     for (int u = 0; u < U; ++u) __builtin_nontemporal_store(x[u] + y[u], d + i + u * B);
   } else {
@@ -80,7 +96,7 @@ extern "C" int tl_clock_khz(int* khz) {
 // shape 0: 512x2 (shipped below 128 MiB per operand), 1: 1024x1 (shipped from 256 MiB); 2, 3: the same, SWAP
 extern "C" unsigned tl_grid(int shape, size_t n) {
   const size_t tiles = (n / 2 + 1023) / 1024;   // 512 x 2 and 1024 x 1: 1024 vectors per block either way
-  return (unsigned)(shape >= 2 ? (tiles + 15) / 16 * 16 : tiles);   // swapped shapes permute within 16
+  return (unsigned)(shape == 2 || shape == 3 ? (tiles + 15) / 16 * 16 : tiles);   // swapped shapes permute within 16
 }
 
 extern "C" int tl_launch(int shape, double* d, const double* s, size_t n, unsigned long long* ts, void* stream,
@@ -101,6 +117,12 @@ extern "C" int tl_launch(int shape, double* d, const double* s, size_t n, unsign
                           (const f64x2*)s, nvec, ts);
   else if (shape == 3)
     hipExtLaunchKernelGGL((k_reduce_tl<1024, 1, true>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
+                          (const f64x2*)s, nvec, ts);
+  else if (shape == 4)   // 1024 x 1, loads only
+    hipExtLaunchKernelGGL((k_reduce_tl<1024, 1, false, 1>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
+                          (const f64x2*)s, nvec, ts);
+  else if (shape == 5)   // 1024 x 1, stores only
+    hipExtLaunchKernelGGL((k_reduce_tl<1024, 1, false, 2>), dim3(grid), dim3(1024), 0, st, a, b, 0, (f64x2*)d,
                           (const f64x2*)s, nvec, ts);
   else
     return -1;
