@@ -1,0 +1,177 @@
+"""The default one-node transport (PG_TRANSPORT=xgmi) at BASELINE's full sizes,
+with REAL processes (one rank per process, all on the test box's one GPU):
+
+  config 3: 4 ranks, int32 sum, 1 GiB per rank (count 2^28)
+  config 4: 8 ranks, double sum, 4 GiB per rank (count 2^29)
+  config 5: 8 ranks, double / int32 product, 4 KiB calls around 2 GiB calls
+  the API's largest count: 2 ranks, int32 sum, INT_MAX elements (8 GiB per rank)
+
+in the auto mode (the library's default: read or push, chosen at connect by
+the link probe) and with push forced.  At these sizes the C oracle would need
+minutes, so each rank computes its expected block on the GPU from the same
+inputs, in the fold order the oracle restates (orc_ring_step, part g of block
+b: x[b+d] op x[b+2d] op ... op x[b]), one IEEE operation per element and step,
+as tests/test_full_size_gpu.py does for the ring executor.  Every rank makes
+every rank's input from a counter-based formula of (rank, index), so no input
+crosses processes except through the transport.  The doubles carry full
+53-bit mantissas, so a different fold order would change their bits."""
+import os
+import pathlib
+import socket
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+CHUNK = 1 << 26          # elements generated per step (bounds the int64 index temporaries)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fill(torch, out, q, off, dt, op):
+    """out[k] = rank q's input at index off + k (deterministic, chunked)."""
+    n = out.numel()
+    for lo in range(0, n, CHUNK):
+        hi = min(n, lo + CHUNK)
+        i = torch.arange(off + lo, off + hi, dtype=torch.int64, device="cuda")
+        h1 = (i * 2654435761 + (q + 1) * 40503) & 0xFFFFFFFF
+        h2 = (i * 2246822519 + (q + 7) * 97) & 0xFFFFFFFF
+        if dt == 0:                           # int32: the full range, wrapping sums and products
+            out[lo:hi] = (h1 - (h1 >= 2**31).to(torch.int64) * 2**32).to(torch.int32)
+        elif op == 0:                         # double sum: full mantissas in [-1, 1)
+            out[lo:hi] = (h1.double() / 2**31 - 1) * (1 + h2.double() / 2**33)
+        else:                                 # double product: 1 + [-2^-10, 2^-10), normal over 8 factors
+            out[lo:hi] = 1 + (h1.double() / 2**31 - 1) * (1 + h2.double() / 2**33) * 2.0**-10
+        del i, h1, h2
+
+
+def _expected(torch, world, rank, count, dt, op, rings, ring_step, block_range):
+    off, ln = block_range(count, world, rank)
+    tdt = torch.int32 if dt == 0 else torch.float64
+    parts = [torch.empty(ln, dtype=tdt, device="cuda") for _ in range(world)]
+    for q in range(world):
+        _fill(torch, parts[q], q, off, dt, op)
+    out = torch.empty(ln, dtype=tdt, device="cuda")
+    for g in range(rings):
+        lo, hi = -(-g * ln // rings), -(-(g + 1) * ln // rings)
+        if lo == hi:
+            continue
+        d = ring_step(world, rings, g) % world
+        acc = parts[(rank + d) % world][lo:hi].clone()
+        for j in range(2, world + 1):
+            src = parts[(rank + j * d) % world][lo:hi]
+            if op == 0:
+                acc.add_(src)
+            else:
+                acc.mul_(src)
+        out[lo:hi] = acc
+        del acc
+    del parts
+    return out
+
+
+def _worker(rank, world, port, q, calls, mode):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="120000")
+    if mode:
+        os.environ["PG_XGMI_MODE"] = mode
+    else:
+        os.environ.pop("PG_XGMI_MODE", None)
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    fails = []
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        if lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h)) != 0:
+            q.put((rank, ["connect: " + pgamd.last_error()]))
+            return
+        rings = int(os.environ.get("PG_RINGS", "2"))
+        for i, (dt, op, count) in enumerate(calls):
+            tdt = torch.int32 if dt == 0 else torch.float64
+            x = torch.empty(count, dtype=tdt, device="cuda")
+            _fill(torch, x, rank, 0, dt, op)
+            off, ln = pgamd.block_range(count, world, rank)
+            out = torch.empty(max(ln, 1), dtype=tdt, device="cuda")
+            torch.cuda.synchronize()
+            if lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, op, h) != 0:
+                fails.append((i, "rc", pgamd.last_error()))
+                break
+            del x
+            want = _expected(torch, world, rank, count, dt, op, rings, orc.ring_step, pgamd.block_range)
+            got = out[:ln]
+            if dt == 1:                          # bits, not values (-0.0 == 0.0)
+                got, want = got.view(torch.int64), want.view(torch.int64)
+            if not torch.equal(got, want):
+                bad = int((got != want).sum())
+                fails.append((i, dt, op, count, f"{bad} of {ln} elements differ"))
+            st = pgamd.stats(h)
+            if st["calls_redone"]:
+                fails.append((i, "call redone with the slot copy"))
+            del out, want, got
+            torch.cuda.empty_cache()
+        lib.pg_close(h)
+    except Exception as e:  # report, never hang the parent
+        fails.append(("exception", repr(e)))
+    q.put((rank, fails))
+
+
+def _run(world, calls, mode, timeout=280):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, calls, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("mode", [None, "push"])
+def test_xgmi_config3_full_size(gpu, mode):
+    _run(4, [(0, 0, 1 << 28)], mode)
+
+
+@pytest.mark.parametrize("mode", [None, "push"])
+def test_xgmi_config4_full_size(gpu, mode):
+    _run(8, [(1, 0, 1 << 29)], mode)
+
+
+def test_xgmi_config5_sequence(gpu):
+    """double and int32 products: 4 KiB (eager size), 2 GiB, 4 KiB, on one handle per process."""
+    calls = []
+    for dt, big in ((1, 1 << 28), (0, 1 << 29)):
+        small = 4096 // (8 if dt == 1 else 4)
+        calls += [(dt, 1, small), (dt, 1, big), (dt, 1, small)]
+    _run(8, calls, None)
+
+
+def test_xgmi_maximum_count(gpu):
+    """INT_MAX int32 elements per rank (8 GiB): every offset past 2^31 and 2^32
+    bytes, the ragged second block (one element shorter)."""
+    _run(2, [(0, 0, (1 << 31) - 1)], None)
