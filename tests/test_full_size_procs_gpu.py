@@ -1,13 +1,16 @@
-"""The default one-node transport (PG_TRANSPORT=xgmi) at BASELINE's full sizes,
-with REAL processes (one rank per process, all on the test box's one GPU):
+"""The W > 1 transports at BASELINE's full sizes with REAL processes (one rank
+per process, all on the test box's one GPU): the default one-node transport
+(PG_TRANSPORT=xgmi) and the RCCL transport (its direct exchange, the one-node
+default, and the two-ring P2P ring; RCCL carries the hops over its socket
+transport here, one NCCL_HOSTID per rank, as in tests/test_rccl_gpu.py):
 
   config 3: 4 ranks, int32 sum, 1 GiB per rank (count 2^28)
   config 4: 8 ranks, double sum, 4 GiB per rank (count 2^29)
   config 5: 8 ranks, double / int32 product, 4 KiB calls around 2 GiB calls
   the API's largest count: 2 ranks, int32 sum, INT_MAX elements (8 GiB per rank)
 
-in the auto mode (the library's default: read or push, chosen at connect by
-the link probe) and with push forced.  At these sizes the C oracle would need
+xgmi in the auto mode (the library's default: read or push, chosen at connect
+by the link probe) and with push forced.  At these sizes the C oracle would need
 minutes, so each rank computes its expected block on the GPU from the same
 inputs, in the fold order the oracle restates (orc_ring_step, part g of block
 b: x[b+d] op x[b+2d] op ... op x[b]), one IEEE operation per element and step,
@@ -77,13 +80,20 @@ def _expected(torch, world, rank, count, dt, op, rings, ring_step, block_range):
     return out
 
 
-def _worker(rank, world, port, q, calls, mode):
-    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="120000")
-    if mode:
-        os.environ["PG_XGMI_MODE"] = mode
-    else:
-        os.environ.pop("PG_XGMI_MODE", None)
+def _env(transport, rank, port, mode=None, algo=None):
+    env = dict(PG_TRANSPORT=transport, PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+               PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="120000", PG_XGMI_MODE=mode, PG_ALGO=algo)
+    if transport == "rccl":
+        env.update(NCCL_HOSTID=f"pg-full-size-{port}-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    return env
+
+
+def _worker(rank, world, port, q, calls, transport, mode, algo):
+    for k, v in _env(transport, rank, port, mode, algo).items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     fails = []
     try:
@@ -130,12 +140,12 @@ def _worker(rank, world, port, q, calls, mode):
     q.put((rank, fails))
 
 
-def _run(world, calls, mode, timeout=280):
+def _run(world, calls, mode=None, transport="xgmi", algo=None, timeout=280):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, calls, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, calls, transport, mode, algo)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
@@ -168,10 +178,21 @@ def test_xgmi_config5_sequence(gpu):
     for dt, big in ((1, 1 << 28), (0, 1 << 29)):
         small = 4096 // (8 if dt == 1 else 4)
         calls += [(dt, 1, small), (dt, 1, big), (dt, 1, small)]
-    _run(8, calls, None)
+    _run(8, calls)
 
 
 def test_xgmi_maximum_count(gpu):
     """INT_MAX int32 elements per rank (8 GiB): every offset past 2^31 and 2^32
     bytes, the ragged second block (one element shorter)."""
-    _run(2, [(0, 0, (1 << 31) - 1)], None)
+    _run(2, [(0, 0, (1 << 31) - 1)])
+
+
+@pytest.mark.parametrize("algo", [None, "ring"])
+def test_rccl_config3_full_size(gpu, algo):
+    """config 3 over RCCL: the direct exchange (default) and the two-ring P2P ring."""
+    _run(4, [(0, 0, 1 << 28)], transport="rccl", algo=algo)
+
+
+def test_rccl_config4_full_size(gpu):
+    """config 4 over RCCL's direct exchange (the one-node default)."""
+    _run(8, [(1, 0, 1 << 29)], transport="rccl")
