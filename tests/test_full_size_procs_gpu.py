@@ -8,6 +8,7 @@ transport here, one NCCL_HOSTID per rank, as in tests/test_rccl_gpu.py):
   config 4: 8 ranks, double sum, 4 GiB per rank (count 2^29)
   config 5: 8 ranks, double / int32 product, 4 KiB calls around 2 GiB calls
   the API's largest count: 2 ranks, int32 sum, INT_MAX elements (8 GiB per rank)
+  pg_all_reduce at configs 3 and 4's sizes, on both transports
 
 xgmi in the auto mode (the library's default: read or push, chosen at connect
 by the link probe) and with push forced.  At these sizes the C oracle would need
@@ -111,28 +112,34 @@ def _worker(rank, world, port, q, calls, transport, mode, algo):
             q.put((rank, ["connect: " + pgamd.last_error()]))
             return
         rings = int(os.environ.get("PG_RINGS", "2"))
-        for i, (dt, op, count) in enumerate(calls):
+        for i, call in enumerate(calls):
+            coll, (dt, op, count) = (call[0], call[1:]) if isinstance(call[0], str) else ("rs", call)
             tdt = torch.int32 if dt == 0 else torch.float64
             x = torch.empty(count, dtype=tdt, device="cuda")
             _fill(torch, x, rank, 0, dt, op)
             off, ln = pgamd.block_range(count, world, rank)
-            out = torch.empty(max(ln, 1), dtype=tdt, device="cuda")
+            out = torch.empty(max(ln, 1) if coll == "rs" else count, dtype=tdt, device="cuda")
             torch.cuda.synchronize()
-            if lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, dt, op, h) != 0:
+            fn = lib.pg_reduce_scatter if coll == "rs" else lib.pg_all_reduce
+            if fn(x.data_ptr(), out.data_ptr(), count, dt, op, h) != 0:
                 fails.append((i, "rc", pgamd.last_error()))
                 break
             del x
-            want = _expected(torch, world, rank, count, dt, op, rings, orc.ring_step, pgamd.block_range)
-            got = out[:ln]
-            if dt == 1:                          # bits, not values (-0.0 == 0.0)
-                got, want = got.view(torch.int64), want.view(torch.int64)
-            if not torch.equal(got, want):
-                bad = int((got != want).sum())
-                fails.append((i, dt, op, count, f"{bad} of {ln} elements differ"))
+            # reduce-scatter: this rank's block; all-reduce: every block, in its own ring order
+            for b in ([rank] if coll == "rs" else range(world)):
+                boff, bln = pgamd.block_range(count, world, b)
+                want = _expected(torch, world, b, count, dt, op, rings, orc.ring_step, pgamd.block_range)
+                got = out[:bln] if coll == "rs" else out[boff:boff + bln]
+                if dt == 1:                          # bits, not values (-0.0 == 0.0)
+                    got, want = got.view(torch.int64), want.view(torch.int64)
+                if not torch.equal(got, want):
+                    bad = int((got != want).sum())
+                    fails.append((i, coll, dt, op, count, b, f"{bad} of {bln} elements differ"))
+                del want, got
             st = pgamd.stats(h)
             if st["calls_redone"]:
                 fails.append((i, "call redone with the slot copy"))
-            del out, want, got
+            del out
             torch.cuda.empty_cache()
         lib.pg_close(h)
     except Exception as e:  # report, never hang the parent
@@ -170,6 +177,15 @@ def test_xgmi_config3_full_size(gpu, mode):
 @pytest.mark.parametrize("mode", [None, "push"])
 def test_xgmi_config4_full_size(gpu, mode):
     _run(8, [(1, 0, 1 << 29)], mode)
+
+
+@pytest.mark.parametrize("transport", ["xgmi", "rccl"])
+def test_all_reduce_full_size(gpu, transport):
+    """pg_all_reduce at configs 3 and 4's sizes (1 GiB int32 over 4 ranks, 4 GiB
+    double over 8): every rank checks every block of its result, each block in
+    its own ring order (the order the reduce-scatter folds it in)."""
+    _run(4, [("ar", 0, 0, 1 << 28)], transport=transport)
+    _run(8, [("ar", 1, 0, 1 << 29)], transport=transport)
 
 
 def test_xgmi_config5_sequence(gpu):
