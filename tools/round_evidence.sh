@@ -11,7 +11,7 @@ tag=${1:-r02}
 part=${2:-all}
 export TMPDIR=/tmp
 if [ "$part" = a ] || [ "$part" = all ]; then
-tools/gpu_step.sh pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+tools/gpu_step.sh pytest_gpu 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread --durations=25
 tools/gpu_step.sh bench 400 python bench.py
 tools/profile_bench.sh "$tag" --steps 50 --warmup 10 --no-host --no-sizes
 tools/gpu_step.sh edge_lab 300 python tools/lab/run_edge_lab.py
