@@ -590,47 +590,60 @@ def _nccl_group():
 def native_crosscheck(lib, h, rank, world, x_full, dt_full):
     """pg_reduce_scatter against RCCL's own reduce-scatter.
 
-    Random inputs (full-range int32, U[-1,1) doubles), 16 Mi elements per rank
-    (a multiple of W, so both libraries use the same uniform blocks).  int32:
-    bit-exact.  double: the two libraries fold the W values in different
-    orders; each sum is within g*sum|x| of the exact one (g = (W-1)u/(1-(W-1)u),
-    u = 2^-53), so |ours - rccl| <= 2*g*sum|x| element-wise, sum|x| taken from
-    an RCCL reduce-scatter of |x|.  Also times RCCL's reduce-scatter on the leg's
+    Random inputs, 16 Mi elements per rank (a multiple of W, so both libraries
+    use the same uniform blocks): full-range int32 for sum and product, U[-1,1)
+    doubles for sum, 1 + U[-2^-10, 2^-10) doubles for product (normal over 8
+    ranks).  int32: bit-exact (wrapping + and * do not depend on the order).
+    double: the two libraries fold the W values in different orders, and each
+    order is within g of the exact result (g = (W-1)u/(1-(W-1)u), u = 2^-53):
+    g*sum|x| for the sum, g*|prod x| for the product.  So |ours - rccl| <=
+    2*g*sum|x| (sum|x| from an RCCL reduce-scatter of |x|) and <= 2*g/(1-g)*|rccl|
+    (product) element-wise.  Also times RCCL's reduce-scatter on the leg's
     full-size input beside ours."""
     import torch.distributed as dist
     grp = _nccl_group()
     n = ((1 << 24) // world) * world
     gen = torch.Generator(device="cuda").manual_seed(777 + rank)
     res = {}
-    for dt in (pgamd.DT_INT32, pgamd.DT_DOUBLE):
+    k = (world - 1) * 2.0**-53
+    g = k / (1 - k)
+    for dt, op in ((pgamd.DT_INT32, pgamd.OP_SUM), (pgamd.DT_DOUBLE, pgamd.OP_SUM),
+                   (pgamd.DT_INT32, pgamd.OP_PROD), (pgamd.DT_DOUBLE, pgamd.OP_PROD)):
+        tag = ("i32_" if dt == pgamd.DT_INT32 else "f64_") + ("sum" if op == pgamd.OP_SUM else "prod")
         if dt == pgamd.DT_INT32:
             x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=gen)
-        else:
+        elif op == pgamd.OP_SUM:
             x = torch.rand(n, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1
+        else:
+            x = 1 + (torch.rand(n, dtype=torch.float64, device="cuda", generator=gen) * 2 - 1) * 2.0**-10
         ln = n // world
         ours = torch.empty(ln, dtype=x.dtype, device="cuda")
         nat = torch.empty(ln, dtype=x.dtype, device="cuda")
+        rop = dist.ReduceOp.SUM if op == pgamd.OP_SUM else dist.ReduceOp.PRODUCT
         torch.cuda.synchronize()
-        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), n, dt, pgamd.OP_SUM, h), "RS")
-        dist.reduce_scatter_tensor(nat, x, group=grp)
+        pgamd.check(lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), n, dt, op, h), "RS")
+        dist.reduce_scatter_tensor(nat, x, op=rop, group=grp)
         torch.cuda.synchronize()
         if dt == pgamd.DT_INT32:
             ok = bool(torch.equal(ours, nat))
-            res["i32_sum_bit_exact"] = sum_over_ranks(1.0 if ok else 0.0, world) == world
+            res[tag + "_bit_exact"] = sum_over_ranks(1.0 if ok else 0.0, world) == world
         else:
-            sabs = torch.empty_like(nat)
-            dist.reduce_scatter_tensor(sabs, x.abs(), group=grp)
-            torch.cuda.synchronize()
-            k = (world - 1) * 2.0**-53
-            tol = 2 * k / (1 - k) * sabs
+            if op == pgamd.OP_SUM:
+                sabs = torch.empty_like(nat)
+                dist.reduce_scatter_tensor(sabs, x.abs(), group=grp)
+                torch.cuda.synchronize()
+                tol = 2 * g * sabs
+            else:
+                tol = 2 * g / (1 - g) * nat.abs()
             diff = (ours - nat).abs()
             worst = float((diff / tol.clamp_min(1e-300)).max())
             ident = float((ours == nat).double().mean())
-            res["f64_sum_within_tol"] = sum_over_ranks(1.0 if worst <= 1.0 else 0.0, world) == world
-            res["f64_max_diff_over_tol"] = round(max_over_ranks(worst, world), 4)
-            res["f64_bit_identical_frac"] = round(sum_over_ranks(ident, world) / world, 4)
-            res["f64_tolerance"] = "|ours - rccl| <= 2*g*sum|x|, g = (W-1)*2^-53/(1-(W-1)*2^-53)"
+            res[tag + "_within_tol"] = sum_over_ranks(1.0 if worst <= 1.0 else 0.0, world) == world
+            res[tag + "_max_diff_over_tol"] = round(max_over_ranks(worst, world), 4)
+            res[tag + "_bit_identical_frac"] = round(sum_over_ranks(ident, world) / world, 4)
         del x, ours, nat
+    res["f64_sum_tolerance"] = "|ours - rccl| <= 2*g*sum|x|, g = (W-1)*2^-53/(1-(W-1)*2^-53)"
+    res["f64_prod_tolerance"] = "|ours - rccl| <= 2*g/(1-g)*|rccl|, g as above"
     # RCCL's own reduce-scatter on the leg's full input, timed like ours
     m = (x_full.numel() // world) * world
     nat = torch.empty(m // world, dtype=x_full.dtype, device="cuda")

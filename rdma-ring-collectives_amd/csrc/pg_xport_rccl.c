@@ -31,13 +31,26 @@ static int rccl_group_start(struct pg_impl *im) {
   return 0;
 }
 
+/* A send or receive that fails inside a group returns -1 to the executor,
+ * which then skips group_end; the group is closed here instead, so the
+ * thread's RCCL group depth is back to zero for the caller's next call. */
+#define PG_CHECK_NCCL_IN_GROUP(expr)                                                    \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess) {                                                            \
+      pg_set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, ncclGetErrorString(r_));  \
+      (void)ncclGroupEnd();                                                             \
+      return -1;                                                                        \
+    }                                                                                   \
+  } while (0)
+
 static int rccl_send(struct pg_impl *im, const void *buf, size_t bytes, int peer, hipStream_t s) {
-  PG_CHECK_NCCL(ncclSend(buf, bytes, ncclUint8, peer, (ncclComm_t)im->xctx, s));
+  PG_CHECK_NCCL_IN_GROUP(ncclSend(buf, bytes, ncclUint8, peer, (ncclComm_t)im->xctx, s));
   return 0;
 }
 
 static int rccl_recv(struct pg_impl *im, void *buf, size_t bytes, int peer, hipStream_t s) {
-  PG_CHECK_NCCL(ncclRecv(buf, bytes, ncclUint8, peer, (ncclComm_t)im->xctx, s));
+  PG_CHECK_NCCL_IN_GROUP(ncclRecv(buf, bytes, ncclUint8, peer, (ncclComm_t)im->xctx, s));
   return 0;
 }
 

@@ -72,6 +72,8 @@ def test_rehearsal_lines_checked_out(world):
         nat = v.get("rccl_native")
         if isinstance(nat, dict):
             assert nat["i32_sum_bit_exact"] and nat["f64_sum_within_tol"]
+            # product rows were added after the round-2 rehearsals; checked when present
+            assert nat.get("i32_prod_bit_exact", True) and nat.get("f64_prod_within_tol", True)
 
 
 def test_batch_launch_at_defaults_above_70_percent():

@@ -45,5 +45,8 @@ def test_native_crosscheck_world1():
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["i32_sum_bit_exact"] is True, res
     assert res["f64_sum_within_tol"] is True, res
-    assert res["f64_bit_identical_frac"] == 1.0, res       # one rank: both are plain copies
+    assert res["i32_prod_bit_exact"] is True, res
+    assert res["f64_prod_within_tol"] is True, res
+    assert res["f64_sum_bit_identical_frac"] == 1.0, res   # one rank: both are plain copies
+    assert res["f64_prod_bit_identical_frac"] == 1.0, res
     assert res["rccl_reduce_scatter_ms"] > 0, res

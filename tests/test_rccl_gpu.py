@@ -265,6 +265,19 @@ def _native_worker(rank, world, port, q, store_port):
         tol = 2 * g / (1 - g) * sabs
         if not bool(((ours - nat).abs() <= tol).all()):
             fails.append(("f64 vs rccl", float((ours - nat).abs().max())))
+        # double product: bit-exact against the oracle's ring, and within
+        # 2g/(1-g) of RCCL's product relative to it (each order is within g of
+        # the exact product; inputs 1 + U[-2^-10, 2^-10) stay normal)
+        xs = [orc.fill(count, 1, 1, 6161 + r) for r in range(world)]
+        want = orc.ring_reduce_scatter(xs, 1, 1, 2)[rank]
+        x = torch.from_numpy(xs[rank]).cuda()
+        assert lib.pg_reduce_scatter(x.data_ptr(), ours.data_ptr(), count, 1, 1, h) == 0, pgamd.last_error()
+        dist.reduce_scatter_tensor(nat, x, op=dist.ReduceOp.PRODUCT)
+        torch.cuda.synchronize()
+        if ours.cpu().numpy().tobytes() != want.tobytes():
+            fails.append(("f64 prod vs oracle",))
+        if not bool(((ours - nat).abs() <= 2 * g / (1 - 2 * g) * nat.abs()).all()):
+            fails.append(("f64 prod vs rccl", float(((ours - nat).abs() / nat.abs()).max())))
         lib.pg_close(h)
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
