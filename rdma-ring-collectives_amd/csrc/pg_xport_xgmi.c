@@ -275,7 +275,8 @@ int pg_xport_xgmi_init(struct pg *pg) {
 
 /* PG_XGMI_MODE=auto: measure, don't guess.  Every rank pulls from all peers
  * at once, then pushes to all peers at once (pgx_xgmi_link_probe, 32 MiB, 3
- * launches per phase); the medians over ranks decide, on every rank alike
+ * launches per phase, two passes, the better of each); the medians over ranks
+ * decide, on every rank alike
  * (one all-gather of the pairs): push when the links move pushed bytes at
  * least 15% faster than pulled ones, else read.  ~1 ms on a node; the probe's
  * exchange slots stay allocated for later calls. */
@@ -288,9 +289,15 @@ static int cmp_double(const void *a, const void *b) {
 static int choose_mode(struct pg *pg) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
-  double g[4] = {0, 0, 0, 0};
-  if (pgx_xgmi_link_probe(pg, XG_PROBE_BYTES, 3, g)) return -1;
-  double mine[2] = {g[2], g[3]}, all[16][2], rd[16], wr[16];
+  /* two passes, the better rate of each direction: a one-off stall in one pass
+   * (another process's work on the links or the GPU) does not decide the mode */
+  double g[4] = {0, 0, 0, 0}, best[2] = {0, 0};
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pgx_xgmi_link_probe(pg, XG_PROBE_BYTES, 3, g)) return -1;
+    if (g[2] > best[0]) best[0] = g[2];
+    if (g[3] > best[1]) best[1] = g[3];
+  }
+  double mine[2] = {best[0], best[1]}, all[16][2], rd[16], wr[16];
   if (pg_boot_allgather(pg, im->boot_fds, mine, all, sizeof(mine))) return -1;
   const int W = pg->world_size;
   for (int q = 0; q < W; ++q) { rd[q] = all[q][0]; wr[q] = all[q][1]; }
