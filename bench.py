@@ -644,6 +644,25 @@ def native_crosscheck(lib, h, rank, world, x_full, dt_full):
         del x, ours, nat
     res["f64_sum_tolerance"] = "|ours - rccl| <= 2*g*sum|x|, g = (W-1)*2^-53/(1-(W-1)*2^-53)"
     res["f64_prod_tolerance"] = "|ours - rccl| <= 2*g/(1-g)*|rccl|, g as above"
+    # the other two collectives on int32 (order-independent, so bit-exact):
+    # pg_all_reduce against RCCL's all-reduce, pg_all_gather against its all-gather
+    x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=gen)
+    ours = torch.empty_like(x)
+    torch.cuda.synchronize()
+    pgamd.check(lib.pg_all_reduce(x.data_ptr(), ours.data_ptr(), n, pgamd.DT_INT32, pgamd.OP_SUM, h), "AR")
+    nat = x.clone()
+    dist.all_reduce(nat, group=grp)
+    torch.cuda.synchronize()
+    res["i32_all_reduce_bit_exact"] = sum_over_ranks(1.0 if torch.equal(ours, nat) else 0.0, world) == world
+    del ours, nat
+    m = n // world
+    ours = torch.empty(m * world, dtype=torch.int32, device="cuda")
+    nat = torch.empty_like(ours)
+    pgamd.check(lib.pg_all_gather(x.data_ptr(), ours.data_ptr(), m, pgamd.DT_INT32, h), "AG")
+    dist.all_gather_into_tensor(nat, x[:m], group=grp)
+    torch.cuda.synchronize()
+    res["i32_all_gather_bit_exact"] = sum_over_ranks(1.0 if torch.equal(ours, nat) else 0.0, world) == world
+    del x, ours, nat
     # RCCL's own reduce-scatter on the leg's full input, timed like ours
     m = (x_full.numel() // world) * world
     nat = torch.empty(m // world, dtype=x_full.dtype, device="cuda")

@@ -74,6 +74,7 @@ def test_rehearsal_lines_checked_out(world):
             assert nat["i32_sum_bit_exact"] and nat["f64_sum_within_tol"]
             # product rows were added after the round-2 rehearsals; checked when present
             assert nat.get("i32_prod_bit_exact", True) and nat.get("f64_prod_within_tol", True)
+            assert nat.get("i32_all_reduce_bit_exact", True) and nat.get("i32_all_gather_bit_exact", True)
 
 
 def test_batch_launch_at_defaults_above_70_percent():

@@ -47,6 +47,8 @@ def test_native_crosscheck_world1():
     assert res["f64_sum_within_tol"] is True, res
     assert res["i32_prod_bit_exact"] is True, res
     assert res["f64_prod_within_tol"] is True, res
+    assert res["i32_all_reduce_bit_exact"] is True, res
+    assert res["i32_all_gather_bit_exact"] is True, res
     assert res["f64_sum_bit_identical_frac"] == 1.0, res   # one rank: both are plain copies
     assert res["f64_prod_bit_identical_frac"] == 1.0, res
     assert res["rccl_reduce_scatter_ms"] > 0, res
