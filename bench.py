@@ -102,6 +102,7 @@ def dist_setup(args):
 
 
 _T0 = time.perf_counter()
+_LEG_INPUT = {}                # (count, dt) -> the ring legs' shared input tensor (ring_leg)
 
 
 def progress(rank, msg):
@@ -856,7 +857,15 @@ def ring_leg(lib, args, rank, world, transport, sink):
             res["rehearsal"] = ("all ranks share one GPU; rccl runs over RCCL's socket transport on loopback "
                                 "(NCCL_HOSTID per rank), xgmi's links are the one device's HBM: rates are not a node's")
         sink[transport] = res          # visible to the watchdog's print while the leg runs
-        x = _pattern(count, rank, world, dt, pgamd.OP_SUM)
+        # every leg reads the SAME input allocation: a fresh tensor after the
+        # previous leg's empty_cache() lands at the freed address under a new HIP
+        # buffer id, and the xgmi transport never exports such a range (DESIGN.md
+        # §5a, "Reused addresses"): the forced-mode legs would then time the slot
+        # copy instead of the zero-copy read they are there to compare
+        x = _LEG_INPUT.get((count, dt))
+        if x is None:
+            _LEG_INPUT.clear()
+            x = _LEG_INPUT[(count, dt)] = _pattern(count, rank, world, dt, pgamd.OP_SUM)
         off, ln = pgamd.block_range(count, world, rank)
         out = torch.empty(max(ln, 1), dtype=x.dtype, device="cuda")
         torch.cuda.synchronize()
