@@ -33,6 +33,8 @@ def build():
            "-fvisibility=hidden", f"-I{ROOT / 'include'}", "-mllvm", "-amdgpu-kernarg-preload-count=16",
            str(ROOT / "rdma-ring-collectives_amd/csrc/pgk_reduce.hip"), "-o", str(SO)]
     subprocess.run(cmd, check=True)
+    for junk in LAB.glob(SO.name + ".0.*"):      # hipcc's offload-bundle leftovers
+        junk.unlink()
 
 
 if "--build" in sys.argv:
