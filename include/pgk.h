@@ -84,6 +84,31 @@ PG_API int pgk_fold_blocks(void *out, const void *const *srcs, int nsrc, size_t 
  * sources may be peer memory) in one launch. */
 PG_API int pgk_gather(void *const *dsts, const void *const *srcs, const size_t *bytes, int k, void *stream);
 
+/* No counterpart in the reference.  For callers that cannot allocate device
+ * memory: code under HIP graph capture, tight serving loops, harnesses that
+ * forbid hipMalloc.  It is the all-reduce of pgx_sim_run(coll =
+ * PG_COLL_ALL_REDUCE) (include/pg_ext.h) over `world` (1 .. 16) device buffers
+ * of the calling process on the current device, with that call's exchange
+ * area (which pgx_sim_run allocates) replaced by a fixed device array inside
+ * the library:
+ *     recvbufs[r][0..count) = the ring all-reduce of sendbufs[0..world)[0..count)
+ * for every r, block b = [b*B, min((b+1)*B, count)), B = ceil(count/world),
+ * part g of `rings` folded in its ring's order (pgk_fold_blocks), so the bits
+ * equal pgx_sim_run's and pg_all_reduce's.  sendbufs[r] == recvbufs[r] (in
+ * place) is allowed; other overlaps are not.  Two launches on `stream`
+ * (inputs -> exchange slots, fold -> every output), asynchronous; it calls no
+ * hipMalloc / hipFree or other allocating routine.
+ * Limit: world * round_up(count * elem_size, 256) <= PGK_STAGED_MAX_BYTES,
+ * else -1 with a message.  Every GPU the library is used on holds that many
+ * bytes from the library's load to the end of the process.
+ * The array's address is resolved once per device by the first call made with
+ * that device current (a count == 0 call does only that; make it outside any
+ * stream capture).  All calls on one GPU share the one array: calls that
+ * overlap in time on the same GPU (different streams or threads) race. */
+#define PGK_STAGED_MAX_BYTES (16u << 20)
+PG_API int pgk_all_reduce_staged(void *const *sendbufs, void *const *recvbufs, int world, size_t count,
+                                 int rings, int dt, int op, void *stream);
+
 /* Device helpers for hosts that do not link HIP themselves (ctypes, cgo ...). */
 PG_API int pgk_device_count(int *count);
 PG_API int pgk_set_device(int device);

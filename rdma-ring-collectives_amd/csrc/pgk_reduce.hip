@@ -249,6 +249,35 @@ __global__ __launch_bounds__(kMultiBlock) void k_fold_blocks(T* __restrict__ out
   }
 }
 
+// k_fold_blocks with the result stored to `nout` buffers at once (every rank
+// of an all-reduce receives the same vector): the fold is computed once per
+// element and written nout times.
+template <typename T>
+struct OutList {
+  T* p[kMaxSrc];
+};
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kMultiBlock) void k_fold_blocks_bcast(OutList<T> out, int nout, SrcList<T> src, int k,
+                                                                   size_t n, size_t block_elems, int rings,
+                                                                   RingSteps steps) {
+  const size_t stride = (size_t)gridDim.x * kMultiBlock;
+  for (size_t i = (size_t)blockIdx.x * kMultiBlock + threadIdx.x; i < n; i += stride) {
+    const int b = (int)(i / block_elems);
+    const size_t b0 = (size_t)b * block_elems;
+    const size_t len = n - b0 < block_elems ? n - b0 : block_elems;
+    const int g = (int)((i - b0) * (size_t)rings / len);
+    const int step = steps.d[g];
+    int q = b + step >= k ? b + step - k : b + step;
+    T acc = src.p[q][i];
+    for (int j = 1; j < k; ++j) {
+      q = q + step >= k ? q + step - k : q + step;
+      acc = apply<OP>(acc, src.p[q][i]);
+    }
+    for (int j = 0; j < nout; ++j) out.p[j][i] = acc;
+  }
+}
+
 // Gather: copy up to 16 byte ranges (one per source rank, possibly peer
 // memory over xGMI) in one launch; blockIdx.y picks the range.  16-byte
 // vectors when a range is 16-B aligned at both ends, else 4-byte words.
@@ -556,6 +585,51 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
 
 }  // namespace
 
+// Exchange area of pgk_all_reduce_staged: one slot per rank.  Every GPU this
+// library runs on holds its own copy of the array, at its own address, until
+// the process ends.  In host code the name is only a handle for
+// hipGetSymbolAddress; launches and copies use the address that call returns.
+static __device__ __align__(256) unsigned char scratch[PGK_STAGED_MAX_BYTES];
+
+namespace {
+
+unsigned char* g_scratch_ptr[kMaxDevices];   // per device, resolved once with that device current
+
+// Device address of `scratch` on the current device (nullptr + message on failure).
+unsigned char* scratch_on_current_device() {
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+    set_err("pgk: staged all-reduce: no usable current device (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (!g_scratch_ptr[dev]) {
+    void* p = nullptr;
+    e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));
+    if (e != hipSuccess || !p) {
+      set_err("pgk: hipGetSymbolAddress(scratch) on device %d: %s", dev, hipGetErrorString(e));
+      return nullptr;
+    }
+    g_scratch_ptr[dev] = (unsigned char*)p;
+  }
+  return g_scratch_ptr[dev];
+}
+
+template <typename T, int OP>
+void launch_fold_bcast(void* const* outs, int nout, const unsigned char* area, size_t slot, int k, size_t n,
+                       size_t block_elems, int rings, const RingSteps& rs, hipStream_t s) {
+  OutList<T> ol{};
+  SrcList<T> sl{};
+  for (int j = 0; j < nout; ++j) ol.p[j] = (T*)outs[j];
+  for (int j = 0; j < k; ++j) sl.p[j] = (const T*)(area + (size_t)j * slot);
+  size_t g = (n + kMultiBlock - 1) / kMultiBlock;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL((k_fold_blocks_bcast<T, OP>), dim3((unsigned)g), dim3(kMultiBlock), 0, s, ol, nout, sl, k, n,
+                     block_elems, rings, rs);
+}
+
+}  // namespace
+
 extern "C" {
 
 int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
@@ -671,6 +745,64 @@ int pgk_gather(void* const* dsts, const void* const* srcs, const size_t* bytes, 
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_gather, dim3((unsigned)g, (unsigned)m), dim3(kMultiBlock), 0, (hipStream_t)stream, cl);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  return 0;
+}
+
+int pgk_all_reduce_staged(void* const* sendbufs, void* const* recvbufs, int world, size_t count, int rings,
+                          int dt, int op, void* stream) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
+  if (world < 1 || world > kMaxSrc) { set_err("pgk: world %d outside 1..%d", world, kMaxSrc); return -1; }
+  if (rings < 1 || rings > kMaxRings) { set_err("pgk: rings %d, expected 1 .. %d", rings, kMaxRings); return -1; }
+  const size_t es = dt == PGK_DT_INT32 ? 4 : 8;
+  if (count > PGK_STAGED_MAX_BYTES / es) {
+    set_err("pgk: staged all-reduce: %zu elements per rank exceed the %zu-byte exchange area", count,
+            (size_t)PGK_STAGED_MAX_BYTES);
+    return -1;
+  }
+  const size_t slot = (count * es + 255) & ~(size_t)255;
+  if (slot * (size_t)world > PGK_STAGED_MAX_BYTES) {
+    set_err("pgk: staged all-reduce: %d ranks x %zu bytes exceed the %zu-byte exchange area (at most %zu bytes "
+            "per rank at this world size)", world, count * es, (size_t)PGK_STAGED_MAX_BYTES,
+            (size_t)PGK_STAGED_MAX_BYTES / (size_t)world / 256 * 256);
+    return -1;
+  }
+  unsigned char* area = scratch_on_current_device();   // also the whole of a count == 0 set-up call
+  if (!area) return -1;
+  if (count == 0) return 0;
+  if (!sendbufs || !recvbufs) { set_err("pgk: NULL buffer list with count=%zu", count); return -1; }
+  for (int q = 0; q < world; ++q)
+    if (!sendbufs[q] || !recvbufs[q] || (((uintptr_t)sendbufs[q] | (uintptr_t)recvbufs[q]) & (es - 1))) {
+      set_err("pgk: staged all-reduce: buffer of rank %d is NULL or not element-aligned", q);
+      return -1;
+    }
+  hipStream_t s = (hipStream_t)stream;
+  // the exchange: every rank's input into its slot, one launch
+  CopyList cl{};
+  for (int q = 0; q < world; ++q) {
+    cl.src[q] = (const char*)sendbufs[q];
+    cl.dst[q] = (char*)(area + (size_t)q * slot);
+    cl.bytes[q] = count * es;
+  }
+  size_t g = (count * es / 16 + kMultiBlock - 1) / kMultiBlock;
+  if (g == 0) g = 1;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)g, (unsigned)world), dim3(kMultiBlock), 0, s, cl);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
+  // the fold, each block in its ring order, stored to every rank's output
+  const size_t blk = (count + (size_t)world - 1) / (size_t)world;
+  RingSteps rs{};
+  for (int p = 0; p < rings; ++p) rs.d[p] = ((ring_step(world, rings, p) % world) + world) % world;
+  if (dt == PGK_DT_INT32) {
+    if (op == PGK_OP_SUM) launch_fold_bcast<uint32_t, PGK_OP_SUM>(recvbufs, world, area, slot, world, count, blk, rings, rs, s);
+    else launch_fold_bcast<uint32_t, PGK_OP_PROD>(recvbufs, world, area, slot, world, count, blk, rings, rs, s);
+  } else {
+    if (op == PGK_OP_SUM) launch_fold_bcast<double, PGK_OP_SUM>(recvbufs, world, area, slot, world, count, blk, rings, rs, s);
+    else launch_fold_bcast<double, PGK_OP_PROD>(recvbufs, world, area, slot, world, count, blk, rings, rs, s);
+  }
+  e = hipGetLastError();
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
   return 0;
 }

@@ -25,6 +25,8 @@ OP_SUM, OP_PROD = 0, 1
 PG_TRANSPORT_RCCL, PG_TRANSPORT_LOOPBACK, PG_TRANSPORT_THREADS, PG_TRANSPORT_SELF, PG_TRANSPORT_XGMI = 0, 1, 2, 3, 4
 PG_BUF_NONE, PG_BUF_SRC, PG_BUF_OUT, PG_BUF_STAGE0, PG_BUF_STAGE1 = 0, 1, 2, 3, 4
 PG_COLL_REDUCE_SCATTER, PG_COLL_ALL_GATHER, PG_COLL_ALL_REDUCE = 0, 1, 2
+# include/pgk.h
+PGK_STAGED_MAX_BYTES = 16 << 20
 
 ELEM_SIZE = {DT_INT32: 4, DT_DOUBLE: 8}
 
@@ -106,6 +108,7 @@ _SIGS = {
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),
+    "pgk_all_reduce_staged": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _SZ, _I, _I, _I, _VP]),
     "pgk_device_count": (_I, [ctypes.POINTER(_I)]),
     "pgk_set_device": (_I, [_I]),
     "pgk_synchronize": (_I, []),
