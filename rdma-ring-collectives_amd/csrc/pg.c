@@ -121,14 +121,25 @@ int pg_stream_wait(hipStream_t s) {
  * it is narrower than a hipDeviceSynchronize(): non-blocking streams of the
  * process that the caller did not order before the call (another thread's
  * work, RCCL's) are not waited for
- * (tests/test_api_gpu.py::test_device_input_behind_slow_producer). */
+ * (tests/test_api_gpu.py::test_device_input_behind_slow_producer).
+ * PG_PRODUCER_SYNC=device restores the reference's fully synchronous contract
+ * (src/pg.c:323-339 is a host call on host memory: whatever produced the
+ * buffers has finished when it is entered): every stream of the device is
+ * waited for at entry, so inputs written on any stream are safe. */
 int pg_wait_producers(struct pg_impl *im, int host_wait) {
   static int skip = -1;                 /* test hook: PG_TEST_SKIP_PRODUCER_WAIT=1 shows the race it prevents */
+  static int device_sync = 0;
   if (skip < 0) {
-    const char *e = getenv("PG_TEST_SKIP_PRODUCER_WAIT");
+    const char *e = getenv("PG_TEST_SKIP_PRODUCER_WAIT"), *m = getenv("PG_PRODUCER_SYNC");
+    if (m && *m && strcmp(m, "device") != 0 && strcmp(m, "null") != 0) {
+      pg_set_error("PG_PRODUCER_SYNC=%s: expected null or device", m);
+      return -1;
+    }
+    device_sync = m && strcmp(m, "device") == 0;
     skip = e && *e == '1';
   }
   if (skip) return 0;
+  if (device_sync) { PG_CHECK_HIP(hipDeviceSynchronize()); return 0; }
   hipError_t q = hipStreamQuery(NULL);
   if (q == hipSuccess) return 0;
   if (q != hipErrorNotReady) { pg_set_error("null stream query: %s", hipGetErrorString(q)); return -1; }
@@ -136,6 +147,7 @@ int pg_wait_producers(struct pg_impl *im, int host_wait) {
   PG_CHECK_HIP(hipEventRecord(im->entry_ev, NULL));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->entry_ev, 0));
   PG_CHECK_HIP(hipStreamWaitEvent(im->red, im->entry_ev, 0));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->red2, im->entry_ev, 0));
   return 0;
 }
 
@@ -256,6 +268,8 @@ int pg_impl_create(struct pg *pg) {
   PG_CHECK_HIP(hipSetDevice(pg->device));
   PG_CHECK_HIP(hipStreamCreateWithFlags(&im->comm, hipStreamNonBlocking));
   PG_CHECK_HIP(hipStreamCreateWithFlags(&im->red, hipStreamNonBlocking));
+  PG_CHECK_HIP(hipStreamCreateWithFlags(&im->red2, hipStreamNonBlocking));
+  PG_CHECK_HIP(hipEventCreateWithFlags(&im->join2_ev, hipEventDisableTiming));
   for (int i = 0; i < PG_RECV_EVENTS; ++i)
     PG_CHECK_HIP(hipEventCreateWithFlags(&im->recv_ev[i], hipEventDisableTiming));
   PG_CHECK_HIP(hipEventCreateWithFlags(&im->join_ev, hipEventDisableTiming));
@@ -274,6 +288,9 @@ int pg_impl_create(struct pg *pg) {
   } else if (pg->hosts && pg_default_transport(pg) == PG_TRANSPORT_XGMI) {
     im->algo = PG_ALGO_DIRECT;                   /* one node, W <= 16: every peer one link away */
   }
+  im->red_bytes = PG_DEFAULT_REDUCE_BYTES;
+  e = getenv("PG_REDUCE_BYTES");
+  if (e && *e) im->red_bytes = (size_t)strtoull(e, NULL, 0);
   im->rings = 2;
   e = getenv("PG_RINGS");
   if (e && *e) {
@@ -288,6 +305,7 @@ void pg_impl_destroy(struct pg *pg) {
   if (!im) return;
   if (im->comm) hipStreamSynchronize(im->comm);
   if (im->red) hipStreamSynchronize(im->red);
+  if (im->red2) hipStreamSynchronize(im->red2);
   if (pg->transport == PG_TRANSPORT_XGMI) pg_xport_xgmi_destroy(pg);
   if (im->ops && im->ops->destroy) im->ops->destroy(im);
   pg_boot_close(im->boot_fds, pg->world_size);
@@ -305,6 +323,9 @@ void pg_impl_destroy(struct pg *pg) {
   if (im->t1) hipEventDestroy(im->t1);
   if (im->comm) hipStreamDestroy(im->comm);
   if (im->red) hipStreamDestroy(im->red);
+  if (im->red2) hipStreamDestroy(im->red2);
+  if (im->join2_ev) hipEventDestroy(im->join2_ev);
+  free(im->pend);
   for (int i = 0; i < 2; ++i) if (im->stage[i]) hipFree(im->stage[i]);
   if (im->dsrc) hipFree(im->dsrc);
   if (im->dout) hipFree(im->dout);
@@ -353,7 +374,20 @@ int connect_process_group(const char *serverlist, void **out_handle) {
 
   if (pg_impl_create(pg)) goto fail;
   if (pg->transport == PG_TRANSPORT_RCCL && pg_xport_rccl_init(pg)) goto fail;
-  if (pg->transport == PG_TRANSPORT_XGMI && pg_xport_xgmi_init(pg)) goto fail;
+  if (pg->transport == PG_TRANSPORT_XGMI) {
+    int rc = pg_xport_xgmi_init(pg);
+    if (rc == 1 && (!tr || !*tr)) {
+      /* xgmi was this library's choice, not the caller's, and the ranks cannot
+       * map each other's memory (every rank learned that together): take the
+       * RCCL transport over the same bootstrap star instead */
+      pg_trace(pg, "xgmi unavailable (%s): falling back to the rccl transport", pg_last_error());
+      pg_xport_xgmi_destroy(pg);
+      pg->transport = PG_TRANSPORT_RCCL;
+      if (pg_xport_rccl_init(pg)) goto fail;
+    } else if (rc) {
+      goto fail;
+    }
+  }
   *out_handle = pg;
   return 0;
 fail:
@@ -424,7 +458,7 @@ void pg_kt_collect(struct pg_impl *im) {
 }
 
 static int sync_ring(struct pg_impl *im, int timed) {
-  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red) || pg_stream_wait(im->red2)) return -1;
   if (timed) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;

@@ -46,11 +46,19 @@ int pg_direct_applies(const struct pg *pg, int count) {
   return im->algo == PG_ALGO_DIRECT && pg->world_size > 1 && pg->world_size <= DIRECT_MAX_WORLD && count > 0;
 }
 
-static int direct_finish(struct pg_impl *im) {
+/* The comm stream observes the last fold of either reduce stream. */
+static int join_folds(struct pg_impl *im) {
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
+  PG_CHECK_HIP(hipEventRecord(im->join2_ev, im->red2));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join2_ev, 0));
+  return 0;
+}
+
+static int direct_finish(struct pg_impl *im) {
+  if (join_folds(im)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
-  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red) || pg_stream_wait(im->red2)) return -1;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
   pg_kt_collect(im);
@@ -82,6 +90,13 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
   for (int g = 0; g < im->rings; ++g) dsteps[g] = pg_ring_offset(W, im->rings, g);
 
   PG_CHECK_HIP(hipEventRecord(im->t0, im->comm));
+  /* Transfers go out batch by batch; the folds of the landed batches wait until
+   * red_bytes per source are pending (PG_REDUCE_BYTES) or the plan ends, and
+   * then each ring's pending segments -- neighbours in every slot -- fold in one
+   * launch.  The gather slots are never reused inside a call, so nothing waits
+   * for a fold, and the fold launches alternate between two streams. */
+  int64_t pend_bytes = 0;
+  int pend_from = 0;                                    /* plan steps [pend_from, j) hold the pending folds */
   int i = 0, nb = 0;
   while (i < n) {
     int j = i;
@@ -97,30 +112,52 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
         return -1;
       im->stats.bytes_sent += st[t].send_bytes;
       im->stats.bytes_recv += st[t].recv_bytes;
+      if (st[t].red_fold) pend_bytes += st[t].red_elems * (int64_t)es;
     }
     if (im->ops->group_end(im, im->comm)) return -1;
-    hipEvent_t rev = im->recv_ev[nb++ % PG_RECV_EVENTS];
-    PG_CHECK_HIP(hipEventRecord(rev, im->comm));
-    PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-    for (int t = i; t < j; ++t) {
-      if (!st[t].red_fold) continue;
-      const size_t o = (size_t)st[t].red_src_off / es, len = (size_t)st[t].red_elems;
-      const void *srcs[DIRECT_MAX_WORLD];
-      for (int k = 0; k < W; ++k) {
-        const int q = ((r + (k + 1) * dsteps[st[t].seg]) % W + W) % W;   /* k = W-1: q = r */
-        srcs[k] = q == r ? (const void *)(src + (boff + o) * es) : (const void *)(gat + ((size_t)q * full + o) * es);
+    if (pend_bytes && ((size_t)pend_bytes >= im->red_bytes || j == n)) {
+      hipEvent_t rev = im->recv_ev[nb++ % PG_RECV_EVENTS];
+      PG_CHECK_HIP(hipEventRecord(rev, im->comm));
+      PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
+      PG_CHECK_HIP(hipStreamWaitEvent(im->red2, rev, 0));
+      for (int g = 0; g < im->rings; ++g) {
+        int t = pend_from;
+        while (t < j) {
+          if (!st[t].red_fold || st[t].seg != g) { ++t; continue; }
+          /* a run of ring g's fold steps, contiguous in the block */
+          int64_t len = st[t].red_elems;
+          int u = t + 1;
+          for (; u < j; ++u) {
+            if (!st[u].red_fold || st[u].seg != g) continue;
+            if (st[u].red_src_off != st[t].red_src_off + len * (int64_t)es ||
+                st[u].red_dst_off != st[t].red_dst_off + len * (int64_t)es)
+              break;
+            len += st[u].red_elems;
+          }
+          if (!len) { t = u; continue; }                 /* empty segments of a short last block */
+          const size_t o = (size_t)st[t].red_src_off / es;
+          const void *srcs[DIRECT_MAX_WORLD];
+          for (int k = 0; k < W; ++k) {
+            const int q = ((r + (k + 1) * dsteps[g]) % W + W) % W;   /* k = W-1: q = r */
+            srcs[k] = q == r ? (const void *)(src + (boff + o) * es) : (const void *)(gat + ((size_t)q * full + o) * es);
+          }
+          void *t0 = NULL, *t1 = NULL;
+          if (im->kt_on) {
+            if (pg_kt_pair(im, &t0, &t1)) return -1;
+            im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * (size_t)len * es);
+          }
+          hipStream_t rs = (im->red_turn++ & 1) ? im->red2 : im->red;
+          if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, (size_t)len, dt, op, (void *)rs, t0, t1)) {
+            pg_set_error("direct: %s", pgk_last_error());
+            return -1;
+          }
+          im->stats.reduce_launches++;
+          im->stats.reduce_elems += len * (W - 1);
+          t = u;
+        }
       }
-      void *t0 = NULL, *t1 = NULL;
-      if (im->kt_on) {
-        if (pg_kt_pair(im, &t0, &t1)) return -1;
-        im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * len * es);
-      }
-      if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, len, dt, op, (void *)im->red, t0, t1)) {
-        pg_set_error("direct: %s", pgk_last_error());
-        return -1;
-      }
-      im->stats.reduce_launches++;
-      im->stats.reduce_elems += (int64_t)len * (W - 1);
+      pend_bytes = 0;
+      pend_from = j;
     }
     i = j;
   }
@@ -219,8 +256,7 @@ int pg_direct_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count,
    * block element by element before writing it, and the sends read the other
    * blocks only */
   if (direct_rs_core(pg, work, work + boff * es, count, dt, op)) return -1;
-  PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
-  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));   /* the gather sends the folded block */
+  if (join_folds(im)) return -1;                                /* the gather sends the folded block */
   if (direct_gather_core(pg, work, count, 0, dt) || direct_finish(im)) return -1;
   if (!rd && pg_timed_copy(recvbuf, work, bytes, &im->stats.d2h_us)) return -1;
   return 0;

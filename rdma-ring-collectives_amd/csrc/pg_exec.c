@@ -1,17 +1,32 @@
 /*
  * pg_exec.c -- executes a ring plan (pg_plan.c) on one rank.
  *
- * Two HIP streams per rank:
- *   comm : transport groups (RCCL ncclSend/ncclRecv over xGMI), in plan order
- *   red  : pgk_reduce of each arrived segment
+ * Streams per rank:
+ *   comm       : transport groups (RCCL ncclSend/ncclRecv over xGMI), in plan order
+ *   red, red2  : the reduce launches, alternating (every launch is independent
+ *                of the previous one: other segments), so one launch's drain
+ *                overlaps the next one's ramp
  * and two kinds of events:
  *   recv_ev[batch]  comm -> red : the batch's segments have landed
  *   red_ev[seg]     red -> comm : the segment's partial is reduced and may be
  *                                 forwarded in the next round
- * so segment j of round k+1 is on the wire while segment j+1 of round k is
- * still being reduced.  This is the pipelining that the reference describes
+ * so segment j of round k+1 is on the wire while later segments of round k
+ * are still arriving.  This is the pipelining that the reference describes
  * for its RDMA path (README.md:17,74-77) and mocks with one synchronous local
  * call per chunk (src/pg.c:276-289).
+ *
+ * The link segment and the reduce launch are separate sizes.  A transport
+ * group carries chunk_bytes x inflight per ring (what the links like); the
+ * arrived segments of a round wait until red_bytes per operand are pending
+ * (PG_REDUCE_BYTES, default 128 MiB) or the round ends, and are then reduced
+ * by ONE pgk_reduce_ranges launch, one contiguous range per ring.  A launch of
+ * that size streams at 80-82% of the HBM peak where a 32 MiB one reaches
+ * 71-73%.  Forwarding is not held up: a round's first sends need the previous
+ * round's first launch only, which ran long before the round's last arrival.
+ *
+ * Every ordering between a reduce and anything else goes through the comm
+ * stream (recv_ev before, red_ev after), never through the order of launches
+ * on a reduce stream, which is what lets two of them alternate.
  *
  * Buffer reuse is safe by construction: a staging segment is overwritten by a
  * receive two rounds later, which the comm stream orders after the send of
@@ -99,11 +114,11 @@ int pg_kt_pair(struct pg_impl *im, void **t0, void **t1) {
   return 0;
 }
 
-static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op) {
+static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op, hipStream_t rs) {
   if (!rb->k) return 0;
   void *t0 = NULL, *t1 = NULL;
   if (im->kt_on && pg_kt_pair(im, &t0, &t1)) return -1;
-  if (pgk_reduce_ranges(rb->out, rb->a, rb->b, rb->n, rb->k, dt, op, (void *)im->red, t0, t1)) {
+  if (pgk_reduce_ranges(rb->out, rb->a, rb->b, rb->n, rb->k, dt, op, (void *)rs, t0, t1)) {
     pg_set_error("pg_exec: %s", pgk_last_error());
     return -1;
   }
@@ -111,6 +126,67 @@ static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op) {
   if (im->kt_on)
     for (int j = 0; j < rb->k; ++j) im->stats.red_kernel_bytes += (int64_t)(3 * rb->n[j] * pg_elem_size(dt));
   rb->k = 0;
+  return 0;
+}
+
+/* Pending reduce steps ordered so that neighbours in memory are neighbours in
+ * the list: by operand buffers and direction, then by destination offset. */
+/* qsort has no context argument: the plan being sorted, per calling thread */
+static __thread const struct pg_step *t_sort_steps;
+static int pend_cmp(const void *pa, const void *pb) {
+  const struct pg_step *a = &t_sort_steps[*(const int *)pa], *b = &t_sort_steps[*(const int *)pb];
+  if (a->red_dst_buf != b->red_dst_buf) return a->red_dst_buf < b->red_dst_buf ? -1 : 1;
+  if (a->red_src_buf != b->red_src_buf) return a->red_src_buf < b->red_src_buf ? -1 : 1;
+  if (a->red_rev != b->red_rev) return a->red_rev < b->red_rev ? -1 : 1;
+  if (a->red_dst_off != b->red_dst_off) return a->red_dst_off < b->red_dst_off ? -1 : 1;
+  return 0;
+}
+
+/* Reduce every pending step: the comm stream's position (behind the last
+ * group that carried any of them) gates one of the two reduce streams, runs of
+ * steps contiguous in both operands become one range each -- the segments of
+ * one ring over consecutive batches are neighbours in the same block -- and
+ * all ranges go out in one pgk_reduce_ranges launch (eight ranges at most per
+ * launch).  Then every step's red_ev is recorded behind it. */
+static int reduce_pending(struct pg_impl *im, const struct pg_step *st, int npend, int nb, void *const bufs[5],
+                          int dt, int op) {
+  if (!npend) return 0;
+  hipStream_t rs = (im->red_turn++ & 1) ? im->red2 : im->red;
+  hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
+  PG_CHECK_HIP(hipEventRecord(rev, im->comm));
+  PG_CHECK_HIP(hipStreamWaitEvent(rs, rev, 0));
+  t_sort_steps = st;
+  qsort(im->pend, (size_t)npend, sizeof(int), pend_cmp);
+  struct red_batch rb;
+  rb.k = 0;
+  const int64_t es = pg_elem_size(dt);
+  int u = 0;
+  while (u < npend) {
+    const struct pg_step *s0 = &st[im->pend[u]];
+    int64_t elems = s0->red_elems;
+    int v = u + 1;
+    while (v < npend) {
+      const struct pg_step *s1 = &st[im->pend[v]];
+      if (s1->red_rev != s0->red_rev || s1->red_dst_buf != s0->red_dst_buf || s1->red_src_buf != s0->red_src_buf ||
+          s1->red_dst_off != s0->red_dst_off + elems * es || s1->red_src_off != s0->red_src_off + elems * es)
+        break;
+      elems += s1->red_elems;
+      ++v;
+    }
+    char *dst = at(bufs, s0->red_dst_buf, s0->red_dst_off);
+    const char *src = at(bufs, s0->red_src_buf, s0->red_src_off);
+    /* the arrival is the left operand: dst = dst op src, or with red_rev
+     * (the arrival sits in src) dst = src op dst */
+    rb.out[rb.k] = dst;
+    rb.a[rb.k] = s0->red_rev ? src : dst;
+    rb.b[rb.k] = s0->red_rev ? dst : src;
+    rb.n[rb.k] = (size_t)elems;
+    im->stats.reduce_elems += elems;
+    if (++rb.k == PG_RED_RANGES && red_flush(im, &rb, dt, op, rs)) return -1;
+    u = v;
+  }
+  if (red_flush(im, &rb, dt, op, rs)) return -1;
+  for (u = 0; u < npend; ++u) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[im->pend[u]].seg], rs));
   return 0;
 }
 
@@ -126,11 +202,19 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
   int max_seg = 0;
   for (int i = 0; i < n; ++i) if (st[i].seg > max_seg) max_seg = st[i].seg;
   if (ensure_red_events(im, max_seg + 1)) return -1;
+  if (n > im->pend_cap) {
+    int *pd = (int *)realloc(im->pend, sizeof(int) * (size_t)n);
+    if (!pd) { pg_set_error("pg_exec: out of host memory"); return -1; }
+    im->pend = pd;
+    im->pend_cap = n;
+  }
 
   int rounds = st[n - 1].round + 1;
   if (hook && ensure_round_events(im, rounds)) return -1;
   im->last_round_rec = -1;
-  int i = 0, nb = 0, cur_round = -1;
+  const int64_t es = pg_elem_size(dt);
+  int i = 0, nb = 0, cur_round = -1, npend = 0;
+  int64_t pend_bytes = 0;
   while (i < n) {
     int b = st[i].batch, j = i;
     while (j < n && st[j].batch == b) ++j;          /* steps [i, j) = one batch */
@@ -165,45 +249,17 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
     }
     if (im->ops->group_end(im, im->comm)) return -1;
 
-    int any_red = 0;
-    for (int s = i; s < j; ++s) any_red |= st[s].red_elems > 0;
-    if (any_red) {
-      hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
-      PG_CHECK_HIP(hipEventRecord(rev, im->comm));
-      PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-      /* runs of segments contiguous in both operands (a batch's segments of
-       * one ring are neighbours in the same block), and every run of the batch
-       * -- one per ring -- in one pgk_reduce_ranges launch */
-      struct red_batch rb;
-      rb.k = 0;
-      const int64_t es = pg_elem_size(dt);
-      int s = i;
-      while (s < j) {
-        if (!st[s].red_elems) { ++s; continue; }
-        int e = s + 1;
-        int64_t elems = st[s].red_elems;
-        while (e < j && st[e].red_elems && st[e].red_rev == st[s].red_rev &&
-               st[e].red_dst_buf == st[s].red_dst_buf && st[e].red_src_buf == st[s].red_src_buf &&
-               st[e].red_dst_off == st[s].red_dst_off + elems * es &&
-               st[e].red_src_off == st[s].red_src_off + elems * es) {
-          elems += st[e].red_elems;
-          ++e;
-        }
-        char *dst = at(bufs, st[s].red_dst_buf, st[s].red_dst_off);
-        const char *src = at(bufs, st[s].red_src_buf, st[s].red_src_off);
-        /* the arrival is the left operand: dst = dst op src, or with red_rev
-         * (the arrival sits in src) dst = src op dst */
-        rb.out[rb.k] = dst;
-        rb.a[rb.k] = st[s].red_rev ? src : dst;
-        rb.b[rb.k] = st[s].red_rev ? dst : src;
-        rb.n[rb.k] = (size_t)elems;
-        im->stats.reduce_elems += elems;
-        if (++rb.k == PG_RED_RANGES && red_flush(im, &rb, dt, op)) return -1;
-        s = e;
+    for (int s = i; s < j; ++s)
+      if (st[s].red_elems > 0) {
+        im->pend[npend++] = s;
+        pend_bytes += st[s].red_elems * es;
       }
-      if (red_flush(im, &rb, dt, op)) return -1;
-      for (int t = i; t < j; ++t)
-        if (st[t].red_elems) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[t].seg], im->red));
+    /* reduce now: enough is pending, or the round (or the plan) ends here --
+     * the next round forwards what this one reduced */
+    if (npend && ((size_t)pend_bytes >= im->red_bytes || j == n || st[j].round != st[i].round)) {
+      if (reduce_pending(im, st, npend, nb, bufs, dt, op)) return -1;
+      npend = 0;
+      pend_bytes = 0;
     }
     ++nb;
     i = j;
@@ -213,8 +269,10 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
     im->last_round_rec = cur_round;
     if (hook(im, hook_ctx, pg->world_size - 1)) return -1;   /* after the last round */
   }
-  /* join: the comm stream observes the last reduce */
+  /* join: the comm stream observes the last reduce of either stream */
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
+  PG_CHECK_HIP(hipEventRecord(im->join2_ev, im->red2));
+  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join2_ev, 0));
   return 0;
 }

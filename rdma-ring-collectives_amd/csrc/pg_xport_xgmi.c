@@ -233,6 +233,54 @@ static int ensure(struct pg *pg, int reg, size_t bytes) {
   return 0;
 }
 
+/* Can every rank map device memory of every other rank?  The server list only
+ * says that the ranks share a host; GPUs without peer access to each other, or
+ * processes confined to their own device, would fail at the first exchange.
+ * Each rank exports a small allocation, opens every peer's, closes it again,
+ * and the outcome is all-gathered: 1 = every rank reached every peer, 0 = some
+ * rank could not (the same answer on every rank, nothing left mapped),
+ * -1 = the bootstrap itself failed.  Test hook PG_XGMI_FAIL_REACH=r: rank r
+ * (-1: every rank) reports that it could not. */
+#define XG_REACH_BYTES (2u << 20)
+static int reach_check(struct pg *pg) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const int W = pg->world_size, r = pg->rank;
+  void *probe = NULL;
+  struct xg_export mine, all[16];
+  memset(&mine, 0, sizeof(mine));
+  hipError_t e = hipMalloc(&probe, XG_REACH_BYTES);
+  if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, probe);
+  mine.ok = e == hipSuccess;
+  if (!mine.ok) (void)hipGetLastError();
+  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, sizeof(mine))) {
+    if (probe) hipFree(probe);
+    return -1;
+  }
+  int ok = 1;
+  for (int q = 0; q < W; ++q) ok &= all[q].ok;
+  for (int q = 0; q < W && ok; ++q) {
+    if (q == r) continue;
+    void *p = NULL;
+    e = hipIpcOpenMemHandle(&p, all[q].h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      pg_trace(pg, "xgmi reach check: rank %d's memory does not map here: %s", q, hipGetErrorString(e));
+      ok = 0;
+    } else {
+      hipIpcCloseMemHandle(p);
+    }
+  }
+  const char *h = getenv("PG_XGMI_FAIL_REACH");
+  if (h && *h && (atoi(h) == r || atoi(h) == -1)) ok = 0;
+  /* the all-gather is also the point after which no peer maps my probe */
+  ok = all_ranks_ok(pg, ok);
+  if (probe) hipFree(probe);
+  return ok;
+}
+
+/* Returns 0, -1 (failed), or 1: the ranks cannot reach each other's memory
+ * (agreed by all of them; nothing of the transport is left set up except the
+ * bootstrap star, which the caller may reuse for another transport). */
 int pg_xport_xgmi_init(struct pg *pg) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   if (pg->world_size > 16) { pg_set_error("xgmi transport: at most 16 ranks"); return -1; }
@@ -260,6 +308,12 @@ int pg_xport_xgmi_init(struct pg *pg) {
   x->imp = (struct xg_import *)calloc((size_t)pg->world_size * XG_IMPORTS, sizeof(struct xg_import));
   if (!x->imp) { pg_set_error("xgmi: out of host memory"); return -1; }
   if (!im->boot_fds && pg_boot_open(pg, &im->boot_fds)) return -1;
+  int reach = reach_check(pg);
+  if (reach < 0) return -1;
+  if (!reach) {
+    pg_set_error("xgmi transport: some rank cannot map a peer's device memory (no peer access or IPC between the GPUs)");
+    return 1;
+  }
   const char *nb = getenv("PG_NO_SHM_BARRIER");
   if (!(nb && *nb == '1') && pg_shm_open(pg, im->boot_fds, &x->bar)) return -1;
   /* push mode publishes its per-call flags in the shm page's descriptor table:
@@ -505,6 +559,14 @@ static void release_stale_imports(struct xgmi_ctx *x, int q, unsigned long long 
     }
 }
 
+/* A pushed call reads no peer input: close every large cached mapping, as the
+ * slot-copy path does, so that an input freed by its owner gives its memory
+ * back at the owner's next call whatever path that call takes. */
+static void release_unread_imports(struct pg *pg, struct xgmi_ctx *x) {
+  for (int q = 0; q < pg->world_size; ++q)
+    if (q != pg->rank) release_stale_imports(x, q, 0);
+}
+
 static void drop_imports(struct pg *pg, struct xgmi_ctx *x) {
   if (!x->imp) return;
   for (int i = 0; i < pg->world_size * XG_IMPORTS; ++i)
@@ -668,15 +730,24 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
       srcs[j] = by_rank[q] + (off_elems + po) * es;
       pg_trace(pg, "xgmi fold: part %d source %d = rank %d at %p", g, j, q, srcs[j]);
     }
-    if (pgk_reduce_multi((char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red)) {
+    /* PG_KERNEL_TIMING=1: the fold's own kernel time (pg_stats.red_kernel_us),
+     * as the ring executor stamps its reduce launches */
+    void *t0 = NULL, *t1 = NULL;
+    if (im->kt_on) {
+      if (pg_kt_pair(im, &t0, &t1)) return -1;
+      im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * pl * es);
+    }
+    if (pgk_reduce_multi_timed((char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red, t0, t1)) {
       pg_set_error("xgmi: %s", pgk_last_error());
       return -1;
     }
+    im->stats.reduce_launches += 1;
   }
   if (pg_stream_wait(im->red)) return -1;
+  pg_kt_collect(im);
   pg_trace(pg, "xgmi fold: done");
   im->stats.kernel_us += us_now() - tk;
-  im->stats.reduce_launches += 1;
+  im->stats.reduce_launches += one_launch;
   im->stats.reduce_elems += (int64_t)len * (W - 1);
   im->stats.bytes_recv += (int64_t)(len * es) * (W - 1);
   return 0;
@@ -777,6 +848,7 @@ static int rs_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int d
     if (push_inputs(pg, (const char *)sendbuf, count, dt, can, by_rank, &pushed)) return -1;
     if (pushed) fold_off = 0;                   /* by_rank[q] point at block `rank` itself */
   }
+  if (pushed) release_unread_imports(pg, x);
   if (!pushed && share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, len * es),
                               by_rank, &zc, &fail))
     return -1;
@@ -854,6 +926,7 @@ static int ar_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int d
     if (push_inputs(pg, (const char *)sendbuf, count, dt, can, by_rank, &pushed)) return -1;
     if (pushed) fold_off = 0;
   }
+  if (pushed) release_unread_imports(pg, x);
   if (!pushed && share_inputs(pg, sendbuf, bytes, is_dev(sendbuf), overlaps(sendbuf, bytes, recvbuf, bytes), by_rank,
                               &zc, &fail))
     return -1;
@@ -959,8 +1032,12 @@ int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
   hipEvent_t e0, e1;
   PG_CHECK_HIP(hipEventCreate(&e0));
   PG_CHECK_HIP(hipEventCreate(&e1));
-  int rc = 0;
-  for (int phase = 0; phase < 4 && rc == 0; ++phase) {
+  /* A rank whose launch or event call fails keeps meeting the others at every
+   * phase's barriers (it only skips its launches), and the outcome is agreed at
+   * the end: all ranks fail together instead of the healthy ones waiting out
+   * the barrier timeout for the one that left. */
+  int rc = 0, lost = 0;
+  for (int phase = 0; phase < 4; ++phase) {
     void *dst[16];
     const void *src[16];
     size_t nb[16];
@@ -975,8 +1052,8 @@ int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
       else { dst[k] = slot(x, XG_REG_X, q, 1) + (size_t)my_idx * part; src[k] = slot(x, XG_REG_X, r, 0); }
       nb[k++] = part;
     }
-    if (barrier(pg)) { rc = -1; break; }
-    if (pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
+    if (barrier(pg)) { lost = 1; break; }
+    if (rc == 0 && pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
     if (rc == 0 && (hipEventRecord(e0, im->red) != hipSuccess)) rc = -1;
     for (int i = 0; rc == 0 && i < reps; ++i)
       if (pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
@@ -984,9 +1061,15 @@ int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
     if (rc == 0 && (hipEventRecord(e1, im->red) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
                     hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
       rc = -1;
+    if (rc) (void)hipStreamSynchronize(im->red);   /* whatever was launched has left the slots */
     size_t moved = phase < 2 ? bytes : part * (size_t)(W - 1);
     gbs[phase] = rc == 0 && ms > 0.f ? (double)moved * reps / (ms * 1e-3) / 1e9 : 0.0;
-    if (barrier(pg)) rc = -1;                  /* nobody overwrites a slot a peer still reads */
+    if (barrier(pg)) { lost = 1; break; }      /* nobody overwrites a slot a peer still reads */
+  }
+  if (lost) rc = -1;                           /* a barrier failed: the ranks are no longer in step */
+  else if (!all_ranks_ok(pg, rc == 0) && rc == 0) {
+    pg_set_error("xgmi probe: a peer's probe failed");
+    rc = -1;
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);

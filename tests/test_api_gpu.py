@@ -414,16 +414,22 @@ def test_nan_payloads_all_reduce_matches_reduce_scatter(gpu, lib, oracle, world,
             assert ar_in[r][off:off + ln].tobytes() == rs[r][:ln].tobytes(), (world, rings, op, r, "in place")
 
 
-def _slow_producer_run(lib, torch, oracle, coll, world=4, count=300007):
+def _slow_producer_run(lib, torch, oracle, coll, world=4, count=300007, side=False):
+    """Inputs written behind a long-running kernel, the collective called at
+    once.  side=False: the producer is the null stream (what the library waits
+    for); side=True: a non-blocking torch stream the caller does not synchronise."""
+    import contextlib
     xs = [oracle.fill(count, 1, 0, 9300 + r) for r in range(world)]
     staged = [to_dev(torch, x) for x in xs]
     S = [torch.zeros(count, dtype=torch.float64, device="cuda") for _ in xs]
     n_out = count * world if coll == pgamd.PG_COLL_ALL_GATHER else count
     R = [torch.zeros(n_out, dtype=torch.float64, device="cuda") for _ in xs]
     torch.cuda.synchronize()
-    torch.cuda._sleep(200_000_000)                   # keep the null stream busy ...
-    for s_, st_ in zip(S, staged):
-        s_.copy_(st_)                                # ... and produce the inputs behind it
+    producer = torch.cuda.Stream() if side else None
+    with (torch.cuda.stream(producer) if side else contextlib.nullcontext()):
+        torch.cuda._sleep(200_000_000)                   # keep the producer stream busy ...
+        for s_, st_ in zip(S, staged):
+            s_.copy_(st_)                                # ... and produce the inputs behind it
     sp = (ctypes.c_void_p * world)(*[ptr(t) for t in S])
     rp = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
     assert lib.pgx_sim_run(world, coll, sp, rp, count, 1, 0, 1 << 16, 4096, 4, 2) == 0, pgamd.last_error()
@@ -436,11 +442,10 @@ def _slow_producer_run(lib, torch, oracle, coll, world=4, count=300007):
     return [to_host(torch, R[r])[:want[r].size].tobytes() == want[r].tobytes() for r in range(world)]
 
 
-def test_device_input_behind_slow_producer_needs_the_wait(gpu, lib, oracle, monkeypatch):
-    """The same sequence with the entry wait switched off (test hook
-    PG_TEST_SKIP_PRODUCER_WAIT=1, read once per process: run in a child) gives
-    wrong results: the non-blocking ring streams read the inputs before the
-    null stream has written them.  So the wait is what the test above passes on."""
+def _slow_producer_child(env_extra, side):
+    """_slow_producer_run in a child process (the env knobs are read once per
+    process): returns (ranks whose result matched the oracle, ranks)."""
+    import os
     import subprocess
     import sys
     code = (
@@ -449,16 +454,38 @@ def test_device_input_behind_slow_producer_needs_the_wait(gpu, lib, oracle, monk
         "from oracle.pyoracle import Oracle\n"
         "import test_api_gpu as t\n"
         "torch.cuda.set_device(0)\n"
-        "ok = t._slow_producer_run(pgamd.load(), torch, Oracle(), pgamd.PG_COLL_REDUCE_SCATTER)\n"
+        "ok = t._slow_producer_run(pgamd.load(), torch, Oracle(), pgamd.PG_COLL_REDUCE_SCATTER, side=sys.argv[2] == '1')\n"
         "print('RESULT', sum(ok), len(ok))\n")
-    import os
-    env = dict(os.environ, PG_TEST_SKIP_PRODUCER_WAIT="1")
+    env = dict(os.environ, **env_extra)
     root = str(pathlib.Path(__file__).resolve().parents[1])
-    r = subprocess.run([sys.executable, "-c", code, root], env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, "-c", code, root, "1" if side else "0"], env=env, capture_output=True,
+                       text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1]
     good, total = map(int, line.split()[1:])
+    return good, total
+
+
+def test_device_input_behind_slow_producer_needs_the_wait(gpu, lib, oracle):
+    """The same sequence with the entry wait switched off (test hook
+    PG_TEST_SKIP_PRODUCER_WAIT=1) gives wrong results: the non-blocking ring
+    streams read the inputs before the null stream has written them.  So the
+    wait is what the test below passes on."""
+    good, total = _slow_producer_child({"PG_TEST_SKIP_PRODUCER_WAIT": "1"}, side=False)
     assert good < total, "without the producer wait every rank still matched: the wait would be unnecessary"
+
+
+def test_side_stream_producer_contract(gpu, lib, oracle):
+    """Inputs produced on a non-blocking stream that the caller does not
+    synchronise.  Default contract (only the null stream is waited for): the
+    collective reads them too early and ranks get wrong blocks.  With
+    PG_PRODUCER_SYNC=device the library waits for every stream at entry, as the
+    reference's host-synchronous call would (src/pg.c:323-339), and every rank
+    gets the oracle's bits."""
+    good, total = _slow_producer_child({}, side=True)
+    assert good < total, "a side-stream producer was waited for by default: the documented contract changed"
+    good, total = _slow_producer_child({"PG_PRODUCER_SYNC": "device"}, side=True)
+    assert good == total
 
 
 def test_device_input_behind_slow_producer(gpu, lib, oracle):
@@ -564,3 +591,30 @@ def test_direct_large_and_random(gpu, lib, oracle, monkeypatch):
         for r in range(world):
             assert got[r][:want[r].size].tobytes() == want[r].tobytes(), (i, world, coll, dt, op, count, cb, infl,
                                                                            rings, on_dev, r)
+
+
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("red_bytes", [0, 1 << 20, 3 << 20, 128 << 20])
+def test_reduce_launch_size_is_independent_of_the_segment(gpu, lib, oracle, monkeypatch, algo, red_bytes):
+    """PG_REDUCE_BYTES: the arrived segments of a round are reduced once that
+    many bytes per operand are pending (0: every batch on its own).  Many small
+    transport groups per round (64 KiB segments, 2 in flight), 1-4 rings,
+    reduce-scatter and in-place all-reduce: whatever the launch size, the bits
+    are the oracle ring's."""
+    monkeypatch.setenv("PG_REDUCE_BYTES", str(red_bytes))
+    monkeypatch.setenv("PG_ALGO", algo)
+    world, count, dt, op = 4, (1 << 22) + 12345, 1, 0
+    xs = [oracle.fill(count, dt, op, 8800 + r) for r in range(world)]
+    for rings in (1, 2, 4):
+        want = oracle.ring_reduce_scatter(xs, dt, op, rings)
+        got = sim(lib, gpu, pgamd.PG_COLL_REDUCE_SCATTER, xs, [np.zeros(w.size, NP[dt]) for w in want], count, dt, op,
+                  1 << 16, 4096, 2, True, rings)
+        for r in range(world):
+            assert got[r].tobytes() == want[r].tobytes(), (algo, red_bytes, rings, r, "rs")
+        want = oracle.ring_all_reduce(xs, dt, op, rings)
+        R = [to_dev(gpu, x) for x in xs]
+        ps = (ctypes.c_void_p * world)(*[ptr(t) for t in R])
+        assert lib.pgx_sim_run(world, pgamd.PG_COLL_ALL_REDUCE, ps, ps, count, dt, op, 1 << 16, 4096, 2, rings) == 0, \
+            pgamd.last_error()
+        for r in range(world):
+            assert to_host(gpu, R[r]).tobytes() == want[r].tobytes(), (algo, red_bytes, rings, r, "ar in place")

@@ -296,3 +296,66 @@ def test_collectives_match_rccl_native(gpu, world):
     for rank, fails in results:
         assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _fallback_worker(rank, world, port, q, fail_reach, forced):
+    """Default transport choice (no PG_TRANSPORT) on one host, with the xgmi
+    reach check made to fail on one rank (test hook PG_XGMI_FAIL_REACH)."""
+    env = _rccl_env(rank, port, True)
+    env.pop("PG_TRANSPORT")
+    os.environ.pop("PG_TRANSPORT", None)
+    os.environ.update(env, PG_XGMI_FAIL_REACH=str(fail_reach))
+    if forced:
+        os.environ["PG_TRANSPORT"] = "xgmi"
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    out = {}
+    try:
+        import ctypes
+
+        import torch
+
+        import pgamd
+        from oracle.pyoracle import Oracle
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        orc = Oracle()
+        h = ctypes.c_void_p()
+        out["rc"] = lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h))
+        out["err"] = pgamd.last_error()
+        if out["rc"] == 0:
+            out["transport"] = pgamd.head(h).transport
+            count = 100003
+            xs = [orc.fill(count, 1, 0, 7700 + r) for r in range(world)]
+            want = orc.ring_reduce_scatter(xs, 1, 0, 2)[rank]
+            S = torch.from_numpy(xs[rank]).cuda()
+            R = torch.zeros(want.size, dtype=torch.float64, device="cuda")
+            out["call"] = lib.pg_reduce_scatter(S.data_ptr(), R.data_ptr(), count, 1, 0, h)
+            out["match"] = R.cpu().numpy().tobytes() == want.tobytes()
+            lib.pg_close(h)
+    except Exception as e:  # noqa: BLE001
+        out["exception"] = repr(e)
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world,fail_reach", [(2, 1), (3, 0), (2, -1)])
+def test_default_transport_falls_back_to_rccl(gpu, world, fail_reach):
+    """The server list says "one host", so xgmi is the default; when some rank
+    cannot map a peer's device memory every rank learns it at connect and all
+    of them come up on the RCCL transport instead, with the same results."""
+    import pgamd
+    results, procs = _run(world, _fallback_worker, lambda r: (fail_reach, False))
+    for rank, out in results:
+        assert out.get("rc") == 0, (rank, out)
+        assert out["transport"] == pgamd.PG_TRANSPORT_RCCL, (rank, out)
+        assert out["call"] == 0 and out["match"], (rank, out)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_forced_xgmi_without_reach_fails_on_every_rank(gpu):
+    """PG_TRANSPORT=xgmi is the caller's choice: no silent fallback, and every
+    rank gets -1 from connect_process_group together."""
+    results, procs = _run(2, _fallback_worker, lambda r: (1, True), timeout=180)
+    for rank, out in results:
+        assert out.get("rc") == -1, (rank, out)
+        assert "cannot map a peer" in out["err"], (rank, out)
+    assert all(p.exitcode == 0 for p in procs)
