@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--ring-div", type=int, default=1,
                     help="divide the ring-leg element counts (one-GPU rehearsals over RCCL's socket transport "
                          "only; the driver's runs keep the BASELINE shapes)")
+    ap.add_argument("--time-budget", type=float, default=480.0,
+                    help="seconds since start after which no further optional leg is started (it is recorded as "
+                         "skipped instead); the primary line always prints.  The driver gives one run 600 s")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
@@ -115,6 +118,31 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+_BUDGET_S = None               # --time-budget
+_ELAPSED = {}                  # leg name -> seconds (rank 0's clock; reported under "elapsed_s")
+
+
+def past_budget(world) -> bool:
+    """True once the slowest rank's clock has passed --time-budget: every rank
+    gets the same answer (one max-reduce), so a skipped leg is skipped by all."""
+    if _BUDGET_S is None:
+        return False
+    return max_over_ranks(time.perf_counter() - _T0, world) > _BUDGET_S
+
+
+class leg_clock:
+    """with leg_clock("name"): ... -> _ELAPSED["name"] = seconds spent inside."""
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.t = time.perf_counter()
+
+    def __exit__(self, *exc):
+        _ELAPSED[self.name] = round(_ELAPSED.get(self.name, 0.0) + time.perf_counter() - self.t, 2)
+        return False
 
 
 def max_over_ranks(x: float, world: int) -> float:
@@ -278,13 +306,14 @@ def size_leg(lib, rank, world, reps=20):
             fit[key] = {"t0_us": round(float(t0), 2), "stream_GBps": round(float(1.0 / slope / 1e3), 1)}
     batches = ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     direct = direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
+    piped = pipelined_rows(lib, base, rank, world, reps)
     lib.pgk_event_destroy(stamp[0])
     lib.pgk_event_destroy(stamp[1])
     del pool
     torch.cuda.empty_cache()
     return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
                         "stamped_frac"], "rows": rows, "edge_fit": fit, "ring_batches": batches,
-            "direct_batches": direct,
+            "direct_batches": direct, "two_streams": piped,
             "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
                       "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
                       "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
@@ -292,21 +321,48 @@ def size_leg(lib, rank, world, reps=20):
                       "write dst) against 8000 GB/s"}
 
 
+def _time_launches(launch, e0, e1, stamp, lib, world, reps):
+    """(ms per launch from events bracketing `reps` back-to-back launches, ms of
+    the median kernel-stamped launch), slowest rank."""
+    for i in range(4):
+        launch(i)
+    torch.cuda.synchronize()
+    barrier(world)
+    e0.record(torch.cuda.current_stream())
+    for i in range(reps):
+        launch(i)
+    e1.record(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+    st = []
+    for i in range(8):
+        launch(i, stamp)
+        torch.cuda.synchronize()
+        v = ctypes.c_float()
+        pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
+        st.append(v.value)
+    return ms, max_over_ranks(float(np.median(st)), world)
+
+
 def ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps):
-    """What one reduce launch of the ring executor costs: a batch carries
-    PG_INFLIGHT segments of PG_CHUNK_BYTES for each of PG_RINGS rings, and
-    pg_exec.c reduces all of them with ONE pgk_reduce_ranges launch (each ring's
-    segments are contiguous; different rings work in different blocks).  Timed
-    here alone, on dst/src ranges 64 MiB apart in the 4 GiB pool, rotating, so
-    every launch streams from HBM.  double sum."""
-    import itertools
+    """What one reduce launch of the ring executor costs.  pg_exec.c reduces the
+    arrived segments of a round once PG_REDUCE_BYTES per operand are pending
+    (default 128 MiB, or at the round's end), every ring's contiguous run as one
+    range of ONE pgk_reduce_ranges launch.  Timed here alone, each ring's range
+    in its own region of the 4 GiB pool, rotating, so every launch streams from
+    HBM.  double sum.  First row = the library defaults; the second is a single
+    transport group (4 MiB x 4 inflight x 2 rings), what PG_REDUCE_BYTES=0 or a
+    round that short launches."""
     rows = []
     dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
     VP, SZ = ctypes.c_void_p, ctypes.c_size_t
-    for chunk, inflight, rings in ((4 << 20, 4, 2), (1 << 20, 4, 2), (16 << 20, 4, 2), (4 << 20, 4, 1),
-                                   (4 << 20, 4, 4), (8 << 20, 4, 2), (4 << 20, 8, 2), (64 << 10, 4, 2)):
-        rng = chunk * inflight                    # bytes per ring per launch, per operand
-        stride = 64 << 20                         # one ring's run per 64 MiB "block"
+    for label, rings, rng in (("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings", 2, 64 << 20),
+                              ("one transport group: 4 MiB x 4 inflight x 2 rings", 2, 16 << 20),
+                              ("64 MiB pending, 2 rings", 2, 32 << 20), ("256 MiB pending, 2 rings", 2, 128 << 20),
+                              ("128 MiB, 1 ring", 1, 128 << 20), ("128 MiB, 4 rings", 4, 32 << 20),
+                              ("one group of 1 MiB x 4 x 2 rings", 2, 4 << 20),
+                              ("one group of 64 KiB x 4 x 2 rings", 2, 256 << 10)):
+        stride = max(64 << 20, rng)               # one ring's range per region
         slots = (SWEEP_POOL // (2 * stride)) // rings
 
         def launch(i, ev=(None, None)):
@@ -317,46 +373,31 @@ def ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps):
             if lib.pgk_reduce_ranges(outs, outs, bs, ns, rings, dt, op, sh, ev[0], ev[1]) != 0:
                 raise RuntimeError(pgamd.last_error())
 
-        for i in range(4):
-            launch(i)
-        torch.cuda.synchronize()
-        barrier(world)
-        e0.record(torch.cuda.current_stream())
-        for i in range(reps):
-            launch(i)
-        e1.record(torch.cuda.current_stream())
-        torch.cuda.synchronize()
-        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
-        st = []
-        for i in range(8):
-            launch(i, stamp)
-            torch.cuda.synchronize()
-            v = ctypes.c_float()
-            pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
-            st.append(v.value)
-        sms = max_over_ranks(float(np.median(st)), world)
+        ms, sms = _time_launches(launch, e0, e1, stamp, lib, world, reps)
         traffic = 3 * rng * rings
-        rows.append([chunk, inflight, rings, rng * rings, round(ms * 1e3, 2),
+        rows.append([label, rings, rng * rings, round(ms * 1e3, 2),
                      round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), round(sms * 1e3, 2),
                      round(traffic / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
-    return {"columns": ["chunk_bytes", "inflight", "rings", "bytes_per_operand", "kernel_us", "frac", "stamped_us",
-                        "stamped_frac"], "rows": rows,
-            "note": "one pgk_reduce_ranges launch = one executor batch (rings ranges of chunk_bytes x inflight), "
-                    "double sum; first row = the library defaults"}
+    return {"columns": ["launch", "rings", "bytes_per_operand", "kernel_us", "frac", "stamped_us", "stamped_frac"],
+            "rows": rows,
+            "note": "one pgk_reduce_ranges launch of the ring executor (one range per ring), double sum; first row = "
+                    "the library defaults"}
 
 
 def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
     """What one fold of the direct exchange costs (PG_ALGO=direct, the rccl
-    transport's default on one node): a batch of PG_INFLIGHT segments of
-    PG_CHUNK_BYTES of one ring part, folded from the W = 8 copies of the block
-    (7 received + this rank's own) by ONE pgk_reduce_multi launch; traffic
-    (W+1) x chunk x inflight.  Sources rotate over the 4 GiB pool.  double sum."""
+    transport's default on one node): the landed segments of one ring part,
+    folded from the W = 8 copies of the block (7 received + this rank's own) by
+    ONE pgk_reduce_multi launch once PG_REDUCE_BYTES per source are pending over
+    the rings (default 128 MiB: 64 MiB per ring at 2 rings); traffic (W+1) x
+    bytes per source.  Sources rotate over the 4 GiB pool.  double sum."""
     rows = []
     dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
     VP = ctypes.c_void_p
-    for chunk, inflight in ((4 << 20, 4), (1 << 20, 4), (16 << 20, 4), (4 << 20, 8)):
-        rng = chunk * inflight                    # bytes per source per launch
-        slot = 64 << 20
+    for label, rng in (("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings", 64 << 20),
+                       ("one transport group: 4 MiB x 4 inflight", 16 << 20), ("32 MiB per source", 32 << 20),
+                       ("128 MiB per source", 128 << 20), ("one group of 1 MiB x 4", 4 << 20)):
+        slot = max(64 << 20, rng)
         sets = SWEEP_POOL // (slot * (nsrc + 1))
 
         def launch(i, ev=(None, None)):
@@ -365,32 +406,57 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
             if lib.pgk_reduce_multi_timed(b0 + slot * nsrc, srcs, nsrc, rng // 8, dt, op, sh, ev[0], ev[1]) != 0:
                 raise RuntimeError(pgamd.last_error())
 
-        for i in range(4):
-            launch(i)
-        torch.cuda.synchronize()
-        barrier(world)
-        e0.record(torch.cuda.current_stream())
-        for i in range(reps):
-            launch(i)
-        e1.record(torch.cuda.current_stream())
-        torch.cuda.synchronize()
-        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
-        st = []
-        for i in range(8):
-            launch(i, stamp)
-            torch.cuda.synchronize()
-            v = ctypes.c_float()
-            pgamd.check(lib.pgk_event_elapsed_ms(stamp[0], stamp[1], ctypes.byref(v)), "elapsed")
-            st.append(v.value)
-        sms = max_over_ranks(float(np.median(st)), world)
+        ms, sms = _time_launches(launch, e0, e1, stamp, lib, world, reps)
         traffic = (nsrc + 1) * rng
-        rows.append([chunk, inflight, nsrc, rng, round(ms * 1e3, 2),
+        rows.append([label, nsrc, rng, round(ms * 1e3, 2),
                      round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), round(sms * 1e3, 2),
                      round(traffic / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
-    return {"columns": ["chunk_bytes", "inflight", "sources", "bytes_per_source", "kernel_us", "frac", "stamped_us",
-                        "stamped_frac"], "rows": rows,
-            "note": "one pgk_reduce_multi launch = one direct-exchange fold (W = 8 sources of chunk_bytes x inflight), "
+    return {"columns": ["launch", "sources", "bytes_per_source", "kernel_us", "frac", "stamped_us", "stamped_frac"],
+            "rows": rows,
+            "note": "one pgk_reduce_multi launch = one direct-exchange fold of one ring part (W = 8 sources), "
                     "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults"}
+
+
+def pipelined_rows(lib, base, rank, world, reps=20):
+    """Independent chunk reduces issued the way the ring executor issues them:
+    alternating between two streams, so one launch's drain overlaps the next
+    one's ramp (every reduce inside a collective is independent of the previous
+    one: other segments).  HIP events on the launching stream bracket the fork,
+    `reps` launches and the join.  Rotating over the 4 GiB pool, double sum, all
+    ranks at once, slowest rank."""
+    dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
+    main = torch.cuda.current_stream()
+    side = [torch.cuda.Stream(), torch.cuda.Stream()]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    rows = []
+    for size in (16 << 20, 32 << 20, 64 << 20, 128 << 20, 256 << 20):
+        n, pairs = size // 8, SWEEP_POOL // (2 * size)
+
+        def burst(count):
+            for i in range(count):
+                d = base + 2 * size * (i % pairs)
+                if lib.pgk_reduce(d, d + size, n, dt, op, side[i & 1].cuda_stream) != 0:
+                    raise RuntimeError(pgamd.last_error())
+
+        burst(4)
+        torch.cuda.synchronize()
+        barrier(world)
+        e0.record(main)
+        for s in side:
+            s.wait_event(e0)
+        burst(reps)
+        for s, ev in zip(side, done):
+            ev.record(s)
+            main.wait_event(ev)
+        e1.record(main)
+        torch.cuda.synchronize()
+        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
+        rows.append([size, round(ms * 1e3, 2), round(3 * size / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
+    return {"columns": ["bytes_per_operand", "us_per_launch", "frac"], "rows": rows,
+            "note": f"{reps} independent pgk_reduce launches alternating between two streams (as pg_exec.c issues "
+                    "its reduce launches), events on the launching stream around fork + launches + join; compare "
+                    "kernel_sizes.rows (one stream: every launch waits for the previous one's drain)"}
 
 
 def cpu_baseline(args):
@@ -757,16 +823,60 @@ def _in_ring_reduce(lib, h, x, out, count, dt, rank, world):
                              "max": round(max(per), 1)},
             "frac_min": round(min(per) / HBM_PEAK_GBS, 4),
             "timing": "PG_KERNEL_TIMING=1: each reduce launch kernel-stamped (pgk_reduce_ranges on the ring, "
-                      "pgk_reduce_multi on the direct exchange); algorithmic bytes (3*n*es per ring reduce, "
-                      "(W+1)*n*es per direct fold) / summed kernel time, one untimed reduce-scatter"}
+                      "pgk_reduce_multi on the direct exchange and in the xgmi transport's fold); algorithmic bytes "
+                      "(3*n*es per ring reduce, (W+1)*n*es per fold) / summed kernel time, one untimed reduce-scatter"}
 
 
-def _ring_variant(lib, rank, world, x, out, count, dt, env, port_off):
+SWEEP_COLUMNS = ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes", "is_default", "algo",
+                 "in_ring_reduce_frac"]
+
+
+def _sweep(lib, h, x, out, count, dt, rank, world, knob, values, algo):
+    """One knob of one handle (one schedule) swept: PG_CHUNK_BYTES (config 3)
+    or PG_INFLIGHT (config 4), set through the public struct pg fields as a
+    reference harness would (include/pg.h).  Rows follow the reference's CSV
+    discipline (README.md:85: size, rounds, inflight, time_us, GB/s) plus the
+    knob, the schedule (`algo`) and the roofline fraction of the reduce launches
+    inside that very configuration (one extra untimed call with
+    PG_KERNEL_TIMING=1: slowest rank).  Stops early, marked, when the time
+    budget runs out."""
+    hd = pgamd.head(h)
+    payload = count * pgamd.ELEM_SIZE[dt]
+    default = int(getattr(hd, knob))
+    rows, truncated = [], False
+    for v in values:
+        if past_budget(world):
+            truncated = True
+            break
+        setattr(hd, knob, v)
+        t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
+        frac = _in_ring_reduce(lib, h, x, out, count, dt, rank, world)["frac_min"]
+        rows.append([payload, world - 1, int(hd.inflight), round(t * 1e6, 1), round(payload / t / 1e9, 2),
+                     int(hd.chunk_bytes), int(v == default), algo, frac])
+    setattr(hd, knob, default)
+    return rows, truncated
+
+
+def _sweep_summary(rows, knob_col):
+    """Per schedule: the fastest row and its gain over the default row."""
+    out = {}
+    for algo in sorted({r[7] for r in rows}):
+        mine = [r for r in rows if r[7] == algo]
+        best = max(mine, key=lambda r: r[4])
+        dflt = [r for r in mine if r[6]]
+        out[algo] = {"fastest": best[knob_col], "fastest_GBps": best[4],
+                     "fastest_over_default": round(best[4] / dflt[0][4], 3) if dflt else None,
+                     "in_ring_reduce_frac_at_default": dflt[0][8] if dflt else None}
+    return out
+
+
+def _ring_variant(lib, rank, world, x, out, count, dt, env, port_off, sweep=None):
     """The same timed reduce-scatter on a second handle (and RCCL communicator)
     opened with `env` (PG_ALGO / PG_RINGS): the W-1 round ring beside the
     default direct exchange, one clockwise ring (what the counter-rotating
     second ring buys), four rings (what two more rings of step +3 / -3 add).
-    int32 results are checked against the default handle's."""
+    int32 results are checked against the default handle's.  sweep = (knob,
+    values): also sweep that knob on this handle (rows under "sweep_rows")."""
     keys = ("PG_RINGS", "PG_PORT", "PG_ALGO")
     saved = {k: os.environ.get(k) for k in keys}
     os.environ.update(env)
@@ -787,6 +897,10 @@ def _ring_variant(lib, rank, world, x, out, count, dt, env, port_off):
         if same is not None:
             res["int32_equal_to_default"] = sum_over_ranks(1.0 if same else 0.0, world) == world
         del ref
+        res["in_ring_reduce"] = _in_ring_reduce(lib, h1, x, out, count, dt, rank, world)
+        if sweep:
+            res["sweep_rows"], res["sweep_truncated"] = _sweep(lib, h1, x, out, count, dt, rank, world, sweep[0],
+                                                               sweep[1], env.get("PG_ALGO", "default"))
         return res
     finally:
         if h1.value:
@@ -877,8 +991,10 @@ def ring_leg(lib, args, rank, world, transport, sink):
         wall = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, args.ring_steps, world)
         payload = count * es                       # per rank
         res["last_call_phases"] = _phases(h, rank, world)
-        if not transport.startswith("xgmi"):       # xgmi folds in its own kernels, no executor launches
-            res["in_ring_reduce"] = _in_ring_reduce(lib, h, x, out, count, dt, rank, world)
+        # the reduce launches inside this very call, kernel-stamped: the executor's
+        # (rccl) or the transport's own multi-source fold (xgmi, whose sources are
+        # its peers' memory: on a node this rate is the links', not local HBM's)
+        res["in_ring_reduce"] = _in_ring_reduce(lib, h, x, out, count, dt, rank, world)
         res.update({"ms_per_reduce_scatter": round(wall * 1e3, 3),
                     "algbw_gibs": round(payload / wall / GIB, 2),
                     "busbw_gibs": round(payload * (world - 1) / world / wall / GIB, 2),
@@ -888,124 +1004,132 @@ def ring_leg(lib, args, rank, world, transport, sink):
                     "rings": int(os.environ.get("PG_RINGS", "2"))})
         if core_only:
             return res
-        progress(rank, f"  {transport}: 4 KiB calls")
-        try:
-            res["eager_4KiB"] = _small_calls(lib, h, rank, world)
-        except Exception as e:  # noqa: BLE001 -- a report row, never fatal for the leg
-            res["eager_4KiB"] = {"error": f"{type(e).__name__}: {e}"}
-        if transport == "xgmi":          # (one-GPU rehearsal: every "link" is the same device)
-            progress(rank, f"  {transport}: link probe")
-            res["link_probe"] = _link_probe(lib, h, rank, world)
-        if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
-            variants = [("ring_algo", {"PG_ALGO": "ring", "PG_RINGS": "2"}, 4),
-                        ("one_ring", {"PG_ALGO": "ring", "PG_RINGS": "1"}, 6)]
-            if world >= 5:
-                variants.append(("four_rings", {"PG_ALGO": "ring", "PG_RINGS": "4"}, 8))
-            for key, env, port_off in variants:
-                progress(rank, f"  {transport}: {key} comparison")
+
+        def optional(key, fn):
+            """One optional part of the leg: skipped (and recorded as such) once the
+            time budget is spent, timed, and never fatal for the leg."""
+            if past_budget(world):
+                res[key] = {"skipped": "time budget"}
+                return
+            progress(rank, f"  {transport}: {key}")
+            with leg_clock(f"ring.{transport}.{key}"):
                 try:
-                    res[key] = _ring_variant(lib, rank, world, x, out, count, dt, env, port_off)
-                except Exception as e:  # noqa: BLE001 -- a comparison row, never fatal for the leg
+                    res[key] = fn()
+                except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
                     res[key] = {"error": f"{type(e).__name__}: {e}"}
-        progress(rank, f"  {transport}: RCCL-native cross-check")
-        try:
-            res["rccl_native"] = native_crosscheck(lib, h, rank, world, x, dt)
-        except Exception as e:  # noqa: BLE001 -- reported; the watchdog covers hangs
-            res["rccl_native"] = {"error": f"{type(e).__name__}: {e}"}
-        # host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)
-        progress(rank, f"  {transport}: host-buffer reduce-scatter")
-        xh = x.cpu().numpy()
-        oh = np.empty(max(ln, 1), dtype=xh.dtype)
-        barrier(world)
-        t0 = time.perf_counter()
-        pgamd.check(lib.pg_reduce_scatter(xh.ctypes.data, oh.ctypes.data, count, dt, pgamd.OP_SUM, h), "host RS")
-        barrier(world)
-        th = max_over_ranks(time.perf_counter() - t0, world)
-        res["host_buffers_ms"] = round(th * 1e3, 2)
-        res["host_buffers_ok"] = sum_over_ranks(1.0 if np.array_equal(oh[:ln], out[:ln].cpu().numpy()) else 0.0,
-                                                world) == world
-        del xh, oh
-        rounds = world - 1
-        # the segment and inflight knobs only exist on the point-to-point ring
-        # (the xgmi transport reads whole blocks); each sweep marks the library
-        # default and names the fastest row -- DESIGN.md §10 states the rule
-        # that turns these rows into the next defaults
-        if world == 4 and transport == "rccl":            # config 3: PG_CHUNK_BYTES sweep
-            progress(rank, f"  {transport}: chunk sweep")
-            rows = []
-            default_cb = int(hd.chunk_bytes)
-            for cb in [1 << e for e in range(16, 29)]:          # 64 KiB .. 256 MiB, every power of two
-                hd.chunk_bytes = cb
-                t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
-                rows.append([payload, rounds, int(hd.inflight), round(t * 1e6, 1), round(payload / t / 1e9, 2),
-                             cb, int(cb == default_cb)])
-            hd.chunk_bytes = default_cb
-            best = max(rows, key=lambda r: r[4])
-            res["chunk_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "chunk_bytes",
-                                              "is_default"], "rows": rows,
-                                  "default_chunk_bytes": default_cb, "fastest_chunk_bytes": best[5],
-                                  "fastest_over_default": round(best[4] / next(r[4] for r in rows if r[6]), 3)}
-        if world == 8 and transport == "rccl":            # config 4: PG_INFLIGHT sweep
-            progress(rank, f"  {transport}: inflight sweep")
-            rows = []
-            default_inf = int(hd.inflight)
-            for inf in (1, 2, 4, 8, 16):
-                hd.inflight = inf
-                t = _timed_rs(lib, h, x, out, count, dt, pgamd.OP_SUM, 2, world)
-                rows.append([payload, rounds, inf, round(t * 1e6, 1), round(payload / t / 1e9, 2), int(inf == default_inf)])
-            hd.inflight = default_inf
-            best = max(rows, key=lambda r: r[4])
-            res["inflight_sweep"] = {"columns": ["size", "rounds", "inflight", "time_us", "GB/s", "is_default"],
-                                     "rows": rows, "default_inflight": default_inf, "fastest_inflight": best[2],
-                                     "fastest_over_default": round(best[4] / next(r[4] for r in rows if r[5]), 3)}
+
+        # 1. What BASELINE's configs 3 and 4 name: a RING with a PG_CHUNK_BYTES /
+        # PG_INFLIGHT sweep.  The knobs exist on the point-to-point transport only
+        # (xgmi reads whole blocks), and each sweep runs on both of its schedules:
+        # the direct exchange (this handle, the default on one node) and the W-1
+        # round ring (PG_ALGO=ring, two counter-rotating rings, a second handle).
+        # Every row names its schedule and carries the roofline fraction of the
+        # reduce launches inside it.  DESIGN.md states the rule that turns these
+        # rows into the next defaults.
+        sweep = None
+        if transport == "rccl" and world == 4:
+            sweep = ("chunk_bytes", [1 << e for e in range(16, 29)], "chunk_sweep", 5)   # 64 KiB .. 256 MiB
+        if transport == "rccl" and world == 8:
+            sweep = ("inflight", [1, 2, 4, 8, 16], "inflight_sweep", 2)
+        own_algo = os.environ.get("PG_ALGO") or "direct"       # one node: the library's default schedule
+        if sweep:
+            def default_sweep():
+                rows, cut = _sweep(lib, h, x, out, count, dt, rank, world, sweep[0], sweep[1], own_algo)
+                return {"columns": SWEEP_COLUMNS, "rows": rows, "truncated_by_time_budget": cut}
+            optional(sweep[2], default_sweep)
+        if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
+            optional("ring_algo", lambda: _ring_variant(lib, rank, world, x, out, count, dt,
+                                                        {"PG_ALGO": "ring", "PG_RINGS": "2"}, 4,
+                                                        (sweep[0], sweep[1]) if sweep else None))
+            if sweep and "sweep_rows" in res["ring_algo"]:
+                table = res[sweep[2]] if "rows" in res.get(sweep[2], {}) else {
+                    "columns": SWEEP_COLUMNS, "rows": [], "truncated_by_time_budget": True}
+                table["rows"] = table["rows"] + res["ring_algo"].pop("sweep_rows")
+                table["truncated_by_time_budget"] |= res["ring_algo"].pop("sweep_truncated")
+                res[sweep[2]] = table
+        if sweep and res.get(sweep[2], {}).get("rows"):
+            res[sweep[2]]["by_algo"] = _sweep_summary(res[sweep[2]]["rows"], sweep[3])
+
+        # 2. config 5 (N = 8): products, eager size and 2 GiB mixed
+        if world == 8:
+            def config5():
+                cfg5 = []
+                for dt5, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
+                    big //= max(args.ring_div, 1)              # 2 GiB per rank unless rehearsing
+                    small = 4096 // pgamd.ELEM_SIZE[dt5]
+                    for cnt in (small, big, small):
+                        xv = _pattern(cnt, rank, world, dt5, pgamd.OP_PROD)
+                        o5, l5 = pgamd.block_range(cnt, world, rank)
+                        ov = torch.empty(max(l5, 1), dtype=xv.dtype, device="cuda")
+                        reps = 20 if cnt == small else 2
+                        t = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
+                        good = bool(torch.equal(ov[:l5], _expected_block(cnt, o5, l5, world, dt5, pgamd.OP_PROD)))
+                        good = sum_over_ranks(1.0 if good else 0.0, world) == world
+                        row = {"dtype": "f64" if dt5 == pgamd.DT_DOUBLE else "i32", "count": cnt,
+                               "bytes": cnt * pgamd.ELEM_SIZE[dt5], "time_us": round(t * 1e6, 1), "ok": good}
+                        if cnt == small and transport == "rccl":
+                            # eager one-shot (default) vs the W-1 round ring: eager_max = 0 disables it
+                            hd.eager_max = 0
+                            tr = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
+                            hd.eager_max = 4096
+                            row["time_us_ring_rounds"] = round(tr * 1e6, 1)
+                        cfg5.append(row)
+                        del xv, ov
+                return cfg5
+            optional("config5_prod_mixed", config5)
+
+        # 3. the small calls, the links, the independent cross-check, host buffers
+        optional("eager_4KiB", lambda: _small_calls(lib, h, rank, world))
+        if transport == "xgmi":          # (one-GPU rehearsal: every "link" is the same device)
+            optional("link_probe", lambda: _link_probe(lib, h, rank, world))
+        optional("rccl_native", lambda: native_crosscheck(lib, h, rank, world, x, dt))
+
+        def host_buffers():
+            """The host-memory form of the same call: PCIe-inclusive (H2D + ring + D2H)."""
+            xh = x.cpu().numpy()
+            oh = np.empty(max(ln, 1), dtype=xh.dtype)
+            barrier(world)
+            t0 = time.perf_counter()
+            pgamd.check(lib.pg_reduce_scatter(xh.ctypes.data, oh.ctypes.data, count, dt, pgamd.OP_SUM, h), "host RS")
+            barrier(world)
+            th = max_over_ranks(time.perf_counter() - t0, world)
+            same = np.array_equal(oh[:ln], _expected_block(count, off, ln, world, dt, pgamd.OP_SUM).cpu().numpy())
+            return {"ms": round(th * 1e3, 2), "ok": sum_over_ranks(1.0 if same else 0.0, world) == world}
+        optional("host_buffers", host_buffers)
+
+        # 4. what the second ring and further rings buy (P2P ring schedule)
+        if transport == "rccl" and os.environ.get("PG_RINGS", "2") == "2":
+            optional("one_ring", lambda: _ring_variant(lib, rank, world, x, out, count, dt,
+                                                       {"PG_ALGO": "ring", "PG_RINGS": "1"}, 6))
+            if world >= 5:
+                optional("four_rings", lambda: _ring_variant(lib, rank, world, x, out, count, dt,
+                                                             {"PG_ALGO": "ring", "PG_RINGS": "4"}, 8))
         del x, out
         torch.cuda.empty_cache()
-        if world == 8:                                    # config 5: prod, eager and 2 GiB mixed
-            progress(rank, f"  {transport}: config 5")
-            cfg5 = []
-            for dt5, big in ((pgamd.DT_DOUBLE, 1 << 28), (pgamd.DT_INT32, 1 << 29)):
-                big //= max(args.ring_div, 1)              # 2 GiB per rank unless rehearsing
-                small = 4096 // pgamd.ELEM_SIZE[dt5]
-                for cnt in (small, big, small):
-                    xv = _pattern(cnt, rank, world, dt5, pgamd.OP_PROD)
-                    o5, l5 = pgamd.block_range(cnt, world, rank)
-                    ov = torch.empty(max(l5, 1), dtype=xv.dtype, device="cuda")
-                    reps = 20 if cnt == small else 2
-                    t = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
-                    good = bool(torch.equal(ov[:l5], _expected_block(cnt, o5, l5, world, dt5, pgamd.OP_PROD)))
-                    good = sum_over_ranks(1.0 if good else 0.0, world) == world
-                    row = {"dtype": "f64" if dt5 == pgamd.DT_DOUBLE else "i32", "count": cnt,
-                           "bytes": cnt * pgamd.ELEM_SIZE[dt5], "time_us": round(t * 1e6, 1), "ok": good}
-                    if cnt == small and transport == "rccl":
-                        # eager one-shot (default) vs the W-1 round ring: eager_max = 0 disables it
-                        hd.eager_max = 0
-                        tr = _timed_rs(lib, h, xv, ov, cnt, dt5, pgamd.OP_PROD, reps, world)
-                        hd.eager_max = 4096
-                        row["time_us_ring_rounds"] = round(tr * 1e6, 1)
-                    cfg5.append(row)
-                    del xv, ov
-                    torch.cuda.empty_cache()
-            res["config5_prod_mixed"] = cfg5
         return res
     finally:
         lib.pg_close(h)
 
 
 def main():
+    global _BUDGET_S
     args = parse()
+    _BUDGET_S = args.time_budget if args.time_budget > 0 else None
     rank, world, local = dist_setup(args)
     lib = pgamd.load()
     # the size table first: the primary measurement then starts on a GPU already at its streaming clocks
     sizes = None
     if not args.no_sizes:
         progress(rank, "kernel size table")
-        try:
-            sizes = size_leg(lib, rank, world)
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal for the primary line
-            sizes = {"error": f"{type(e).__name__}: {e}"}
+        with leg_clock("kernel_sizes"):
+            try:
+                sizes = size_leg(lib, rank, world)
+            except Exception as e:  # noqa: BLE001 -- reported, never fatal for the primary line
+                sizes = {"error": f"{type(e).__name__}: {e}"}
 
     progress(rank, f"kernel leg (world {world}, device {local})")
-    wall, region_mean_ms, stamped_ms = kernel_leg(lib, args, rank, world)
+    with leg_clock("kernel_leg"):
+        wall, region_mean_ms, stamped_ms = kernel_leg(lib, args, rank, world)
     wall_max = max_over_ranks(wall, world)
     bytes_per_step = 3 * N_ELEMS * 8
     per_rank_ms = gather_over_ranks(region_mean_ms, rank, world)
@@ -1017,19 +1141,22 @@ def main():
     host = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         progress(rank, "cpu baseline")
-        cpu = cpu_baseline(args)
+        with leg_clock("cpu_baseline"):
+            cpu = cpu_baseline(args)
     if world == 1 and not args.no_host:
         progress(rank, "host-memory leg")
-        try:
-            host = host_leg(lib)
-        except Exception as e:
-            host = {"error": f"{type(e).__name__}: {e}"}
+        with leg_clock("host_staged"):
+            try:
+                host = host_leg(lib)
+            except Exception as e:
+                host = {"error": f"{type(e).__name__}: {e}"}
     cfg1 = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        try:
-            cfg1 = config1_leg(lib)
-        except Exception as e:
-            cfg1 = {"error": f"{type(e).__name__}: {e}"}
+        with leg_clock("config1"):
+            try:
+                cfg1 = config1_leg(lib)
+            except Exception as e:
+                cfg1 = {"error": f"{type(e).__name__}: {e}"}
 
     line = None
     if rank == 0:
@@ -1063,6 +1190,8 @@ def main():
             "config1": cfg1,
             "ring": None,
             "kernel": lib.pgk_version().decode(),
+            "elapsed_s": _ELAPSED,       # per leg, filled in place; "total" is set just before printing
+            "time_budget_s": _BUDGET_S,
         }
 
     if world > 1 and not args.no_ring:
@@ -1078,6 +1207,7 @@ def main():
             if line is not None:
                 ring["watchdog"] = (f"ring leg exceeded {args.ring_timeout} s; the leg that was running is "
                                     "reported up to where it stopped, later ones are omitted")
+                _ELAPSED["total"] = round(time.perf_counter() - _T0, 2)
                 txt = None
                 for _ in range(20):          # the main thread may be adding to the ring dict right now
                     try:
@@ -1097,15 +1227,20 @@ def main():
         dog.daemon = True
         dog.start()
         for transport in args.transports.split(","):
+            if past_budget(world):           # the same answer on every rank
+                ring[transport] = {"skipped": "time budget"}
+                continue
             progress(rank, f"ring leg: {transport}")
-            try:
-                ring_leg(lib, args, rank, world, transport, ring)
-            except Exception as e:  # the primary measurement stands on its own
-                ring.setdefault(transport, {})["error"] = f"{type(e).__name__}: {e}"
+            with leg_clock(f"ring.{transport}"):
+                try:
+                    ring_leg(lib, args, rank, world, transport, ring)
+                except Exception as e:  # the primary measurement stands on its own
+                    ring.setdefault(transport, {})["error"] = f"{type(e).__name__}: {e}"
             barrier(world)
         dog.cancel()
 
     if line is not None:
+        _ELAPSED["total"] = round(time.perf_counter() - _T0, 2)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

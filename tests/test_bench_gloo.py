@@ -12,6 +12,7 @@ import os
 import pathlib
 import socket
 import sys
+import time
 
 import pytest
 import torch.multiprocessing as mp
@@ -42,6 +43,15 @@ def _worker(rank, world, port, q):
         assert bench.gather_over_ranks(10.0 * rank, rank, world) == [10.0 * r for r in range(world)]
         assert bench.sum_over_ranks(1.0, world) == float(world)
         bench.barrier(world)
+        # the time budget: one answer on every rank, decided by the slowest clock
+        # (rank 1 started its clock "200 s ago"; the others just now)
+        bench._T0 = time.perf_counter() - (200.0 if rank == 1 else 0.0)
+        bench._BUDGET_S = None
+        assert bench.past_budget(world) is False
+        bench._BUDGET_S = 100.0
+        assert bench.past_budget(world) is True
+        bench._BUDGET_S = 1000.0
+        assert bench.past_budget(world) is False
         checked = 0
         for dt in (pgamd.DT_INT32, pgamd.DT_DOUBLE):
             for op in (pgamd.OP_SUM, pgamd.OP_PROD):
@@ -79,3 +89,19 @@ def test_bench_expected_blocks_over_gloo(world):
         assert p.exitcode == 0
     for rank, checked, ok in results:
         assert checked == 2 * 2 * 4 * 2 and ok is True, (rank, checked, ok)
+
+
+def test_sweep_summary_names_the_fastest_row_per_schedule():
+    """bench._sweep_summary: per schedule, the fastest row of the knob and its
+    gain over that schedule's default row."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    import bench
+    cols = bench.SWEEP_COLUMNS
+    assert cols[:5] == ["size", "rounds", "inflight", "time_us", "GB/s"] and "algo" in cols
+    rows = [[1 << 30, 3, 4, 100.0, 10.0, 1 << 20, 0, "direct", 0.70], [1 << 30, 3, 4, 50.0, 20.0, 4 << 20, 1, "direct", 0.78],
+            [1 << 30, 3, 4, 40.0, 25.0, 16 << 20, 0, "direct", 0.80], [1 << 30, 3, 4, 90.0, 11.0, 4 << 20, 1, "ring", 0.79],
+            [1 << 30, 3, 4, 80.0, 12.1, 8 << 20, 0, "ring", 0.81]]
+    s = bench._sweep_summary(rows, cols.index("chunk_bytes"))
+    assert s["direct"] == {"fastest": 16 << 20, "fastest_GBps": 25.0, "fastest_over_default": 1.25,
+                           "in_ring_reduce_frac_at_default": 0.78}
+    assert s["ring"]["fastest"] == 8 << 20 and s["ring"]["fastest_over_default"] == 1.1
