@@ -306,14 +306,13 @@ def size_leg(lib, rank, world, reps=20):
             fit[key] = {"t0_us": round(float(t0), 2), "stream_GBps": round(float(1.0 / slope / 1e3), 1)}
     batches = ring_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
     direct = direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps)
-    piped = pipelined_rows(lib, base, rank, world, reps)
     lib.pgk_event_destroy(stamp[0])
     lib.pgk_event_destroy(stamp[1])
     del pool
     torch.cuda.empty_cache()
     return {"columns": ["dtype", "op", "bytes_per_operand", "kernel_us", "GB/s", "frac", "stamped_us",
                         "stamped_frac"], "rows": rows, "edge_fit": fit, "ring_batches": batches,
-            "direct_batches": direct, "two_streams": piped,
+            "direct_batches": direct,
             "timing": f"kernel_us: HIP events bracketing {reps} back-to-back launches rotating over a 4 GiB pool "
                       "(includes the ~1-2 us kernel boundaries), all ranks at once, slowest rank; stamped_us: median "
                       "of 8 kernel-stamped launches (hipExtLaunchKernelGGL events, the kernel alone as rocprofv3 "
@@ -415,48 +414,6 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
             "rows": rows,
             "note": "one pgk_reduce_multi launch = one direct-exchange fold of one ring part (W = 8 sources), "
                     "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults"}
-
-
-def pipelined_rows(lib, base, rank, world, reps=20):
-    """Independent chunk reduces issued the way the ring executor issues them:
-    alternating between two streams, so one launch's drain overlaps the next
-    one's ramp (every reduce inside a collective is independent of the previous
-    one: other segments).  HIP events on the launching stream bracket the fork,
-    `reps` launches and the join.  Rotating over the 4 GiB pool, double sum, all
-    ranks at once, slowest rank."""
-    dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
-    main = torch.cuda.current_stream()
-    side = [torch.cuda.Stream(), torch.cuda.Stream()]
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    done = [torch.cuda.Event(), torch.cuda.Event()]
-    rows = []
-    for size in (16 << 20, 32 << 20, 64 << 20, 128 << 20, 256 << 20):
-        n, pairs = size // 8, SWEEP_POOL // (2 * size)
-
-        def burst(count):
-            for i in range(count):
-                d = base + 2 * size * (i % pairs)
-                if lib.pgk_reduce(d, d + size, n, dt, op, side[i & 1].cuda_stream) != 0:
-                    raise RuntimeError(pgamd.last_error())
-
-        burst(4)
-        torch.cuda.synchronize()
-        barrier(world)
-        e0.record(main)
-        for s in side:
-            s.wait_event(e0)
-        burst(reps)
-        for s, ev in zip(side, done):
-            ev.record(s)
-            main.wait_event(ev)
-        e1.record(main)
-        torch.cuda.synchronize()
-        ms = max_over_ranks(e0.elapsed_time(e1) / reps, world)
-        rows.append([size, round(ms * 1e3, 2), round(3 * size / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
-    return {"columns": ["bytes_per_operand", "us_per_launch", "frac"], "rows": rows,
-            "note": f"{reps} independent pgk_reduce launches alternating between two streams (as pg_exec.c issues "
-                    "its reduce launches), events on the launching stream around fork + launches + join; compare "
-                    "kernel_sizes.rows (one stream: every launch waits for the previous one's drain)"}
 
 
 def cpu_baseline(args):
@@ -762,6 +719,13 @@ def _phases(h, rank, world):
     out["calls_redone_total"] = int(sum_over_ranks(float(st["calls_redone"]), world))
     t = out["kernel_us"] or out["ring_us"]
     out["recv_gbs_per_rank"] = round(st["bytes_recv"] / t / 1e3, 1) if t else None
+    # the data path this handle actually runs, from the library itself (pg_get_stats)
+    names = {pgamd.PG_TRANSPORT_RCCL: "rccl", pgamd.PG_TRANSPORT_XGMI: "xgmi"}
+    out["path"] = {"transport": names.get(st["transport"], str(st["transport"])),
+                   "schedule": ("push" if st["xgmi_push"] else "read") if st["transport"] == pgamd.PG_TRANSPORT_XGMI
+                   else ("direct" if st["algo_direct"] else "ring"),
+                   "chosen_by_probe": bool(st["xgmi_mode_auto"]),
+                   "probe_read_gbs": round(st["probe_read_gbs"], 1), "probe_write_gbs": round(st["probe_write_gbs"], 1)}
     return out
 
 

@@ -180,6 +180,13 @@ struct pg_stats {
                             when PG_KERNEL_TIMING=1 stamps each launch (else 0) */
   int64_t red_kernel_bytes; /* algorithmic HBM bytes of those launches: 3*n*es per
                             ring reduce, (W+1)*n*es per direct fold            */
+  /* which data path this handle runs (constant over the handle's life), so that a
+     record of a run shows it: */
+  int32_t transport;     /* PG_TRANSPORT_* actually in use (RCCL after an xgmi fallback) */
+  int32_t algo_direct;   /* P2P transports: 1 = direct exchange, 0 = W-1 round ring */
+  int32_t xgmi_push;     /* xgmi: 1 = push mode, 0 = read mode                   */
+  int32_t xgmi_mode_auto;/* xgmi: 1 = the mode was chosen by the connect-time probe */
+  double probe_read_gbs, probe_write_gbs;  /* that probe's medians over ranks (0 when forced) */
 };
 PG_API int pg_get_stats(void *pg_handle, struct pg_stats *out);
 

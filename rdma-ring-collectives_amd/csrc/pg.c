@@ -147,7 +147,6 @@ int pg_wait_producers(struct pg_impl *im, int host_wait) {
   PG_CHECK_HIP(hipEventRecord(im->entry_ev, NULL));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->entry_ev, 0));
   PG_CHECK_HIP(hipStreamWaitEvent(im->red, im->entry_ev, 0));
-  PG_CHECK_HIP(hipStreamWaitEvent(im->red2, im->entry_ev, 0));
   return 0;
 }
 
@@ -268,8 +267,6 @@ int pg_impl_create(struct pg *pg) {
   PG_CHECK_HIP(hipSetDevice(pg->device));
   PG_CHECK_HIP(hipStreamCreateWithFlags(&im->comm, hipStreamNonBlocking));
   PG_CHECK_HIP(hipStreamCreateWithFlags(&im->red, hipStreamNonBlocking));
-  PG_CHECK_HIP(hipStreamCreateWithFlags(&im->red2, hipStreamNonBlocking));
-  PG_CHECK_HIP(hipEventCreateWithFlags(&im->join2_ev, hipEventDisableTiming));
   for (int i = 0; i < PG_RECV_EVENTS; ++i)
     PG_CHECK_HIP(hipEventCreateWithFlags(&im->recv_ev[i], hipEventDisableTiming));
   PG_CHECK_HIP(hipEventCreateWithFlags(&im->join_ev, hipEventDisableTiming));
@@ -305,7 +302,6 @@ void pg_impl_destroy(struct pg *pg) {
   if (!im) return;
   if (im->comm) hipStreamSynchronize(im->comm);
   if (im->red) hipStreamSynchronize(im->red);
-  if (im->red2) hipStreamSynchronize(im->red2);
   if (pg->transport == PG_TRANSPORT_XGMI) pg_xport_xgmi_destroy(pg);
   if (im->ops && im->ops->destroy) im->ops->destroy(im);
   pg_boot_close(im->boot_fds, pg->world_size);
@@ -323,8 +319,6 @@ void pg_impl_destroy(struct pg *pg) {
   if (im->t1) hipEventDestroy(im->t1);
   if (im->comm) hipStreamDestroy(im->comm);
   if (im->red) hipStreamDestroy(im->red);
-  if (im->red2) hipStreamDestroy(im->red2);
-  if (im->join2_ev) hipEventDestroy(im->join2_ev);
   free(im->pend);
   for (int i = 0; i < 2; ++i) if (im->stage[i]) hipFree(im->stage[i]);
   if (im->dsrc) hipFree(im->dsrc);
@@ -419,6 +413,7 @@ int pg_close(void *pg_handle) {
   struct pg *pg = (struct pg *)pg_handle;
   if (!pg) return 0;
   pg_impl_destroy(pg);
+  if (g_trace && g_trace != stderr) fflush(g_trace);   /* a host that ends with _exit() keeps its trace */
   if (pg->hosts) {
     for (int i = 0; i < pg->world_size; ++i) free(pg->hosts[i]);
     free(pg->hosts);
@@ -433,6 +428,18 @@ int pg_get_stats(void *pg_handle, struct pg_stats *out) {
   const struct pg_impl *im = (const struct pg_impl *)pg->impl;
   *out = im->stats;
   out->calls_redone = im->calls_redone;
+  out->transport = pg->transport;
+  out->algo_direct = im->algo == PG_ALGO_DIRECT;
+  if (pg->transport == PG_TRANSPORT_XGMI) {
+    int push = 0;
+    double rd = 0, wr = 0;
+    if (pgx_xgmi_mode(pg, &push, &rd, &wr) == 0) {
+      out->xgmi_push = push;
+      out->xgmi_mode_auto = rd > 0 || wr > 0;
+      out->probe_read_gbs = rd;
+      out->probe_write_gbs = wr;
+    }
+  }
   return 0;
 }
 
@@ -458,7 +465,7 @@ void pg_kt_collect(struct pg_impl *im) {
 }
 
 static int sync_ring(struct pg_impl *im, int timed) {
-  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red) || pg_stream_wait(im->red2)) return -1;
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
   if (timed) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
@@ -707,8 +714,8 @@ int pg_reduce_scatter(void *sendbuf, void *recvbuf, int count, DATATYPE datatype
     rc = pg_xgmi_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else if (pg_eager_applies(pg, count, datatype))
     rc = pg_eager_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
-  else if (pg_direct_applies(pg, count))
-    rc = pg_direct_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_direct_applies(pg, count) && (rc = pg_direct_prepare(pg, count, datatype)) != 0)
+    rc = rc < 0 ? -1 : pg_direct_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_reduce_scatter(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;
@@ -899,8 +906,8 @@ int pg_all_reduce(void *sendbuf, void *recvbuf, int count, DATATYPE datatype, OP
     rc = pg_xgmi_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   else if (pg_eager_applies(pg, count, datatype))
     rc = pg_eager_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
-  else if (pg_direct_applies(pg, count))
-    rc = pg_direct_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
+  else if (pg_direct_applies(pg, count) && (rc = pg_direct_prepare(pg, count, datatype)) != 0)
+    rc = rc < 0 ? -1 : pg_direct_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   else
     rc = ring_all_reduce(pg, sendbuf, recvbuf, count, datatype, kop);
   im->stats.wall_us = now_us() - t;

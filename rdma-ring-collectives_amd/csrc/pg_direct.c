@@ -46,19 +46,45 @@ int pg_direct_applies(const struct pg *pg, int count) {
   return im->algo == PG_ALGO_DIRECT && pg->world_size > 1 && pg->world_size <= DIRECT_MAX_WORLD && count > 0;
 }
 
-/* The comm stream observes the last fold of either reduce stream. */
+/* The comm stream observes the last fold. */
 static int join_folds(struct pg_impl *im) {
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
-  PG_CHECK_HIP(hipEventRecord(im->join2_ev, im->red2));
-  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join2_ev, 0));
+  return 0;
+}
+
+/* The gather area holds W full blocks -- as much as the whole input, where the
+ * ring stages about two blocks.  When it has to grow and some rank cannot
+ * allocate it, every rank takes the ring for this call instead (the ranks agree
+ * over the bootstrap star; growth happens in the same call on every rank,
+ * because every rank sees the same counts).  Returns 1: run the direct
+ * exchange, 0: use the ring (agreed by all ranks), -1: failed.  Test hook
+ * PG_TEST_FAIL_STAGE_ALLOC=r: rank r's allocation fails. */
+int pg_direct_prepare(struct pg *pg, int count, int dt) {
+  struct pg_impl *im = (struct pg_impl *)pg->impl;
+  const size_t W = (size_t)pg->world_size, full = ((size_t)count + W - 1) / W;
+  const size_t need = W * full * pg_elem_size(dt);
+  if (im->ebuf && need <= im->ebuf_cap) return 1;
+  int ok = pg_ensure(&im->ebuf, &im->ebuf_cap, need) == 0;
+  const char *h = getenv("PG_TEST_FAIL_STAGE_ALLOC");
+  if (h && *h && atoi(h) == pg->rank) ok = 0;
+  if (!ok) (void)hipGetLastError();
+  if (!im->boot_fds) return ok ? 1 : -1;          /* in-process ranks: nothing to agree over */
+  char mine = (char)ok, all[DIRECT_MAX_WORLD];
+  if (pg_boot_allgather(pg, im->boot_fds, &mine, all, 1)) return -1;
+  for (int q = 0; q < pg->world_size; ++q) ok &= all[q] != 0;
+  if (ok) return 1;
+  /* every rank drops the area, so that all of them see "has to grow" alike next time */
+  if (im->ebuf) { hipFree(im->ebuf); im->ebuf = NULL; }
+  im->ebuf_cap = 0;
+  pg_trace(pg, "direct: %zu bytes of gather area not available on every rank; falling back to the ring", need);
   return 0;
 }
 
 static int direct_finish(struct pg_impl *im) {
   if (join_folds(im)) return -1;
   PG_CHECK_HIP(hipEventRecord(im->t1, im->comm));
-  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red) || pg_stream_wait(im->red2)) return -1;
+  if (pg_stream_wait(im->comm) || pg_stream_wait(im->red)) return -1;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, im->t0, im->t1) == hipSuccess) im->stats.ring_us += (double)ms * 1e3;
   pg_kt_collect(im);
@@ -94,7 +120,7 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
    * red_bytes per source are pending (PG_REDUCE_BYTES) or the plan ends, and
    * then each ring's pending segments -- neighbours in every slot -- fold in one
    * launch.  The gather slots are never reused inside a call, so nothing waits
-   * for a fold, and the fold launches alternate between two streams. */
+   * for a fold. */
   int64_t pend_bytes = 0;
   int pend_from = 0;                                    /* plan steps [pend_from, j) hold the pending folds */
   int i = 0, nb = 0;
@@ -119,7 +145,6 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
       hipEvent_t rev = im->recv_ev[nb++ % PG_RECV_EVENTS];
       PG_CHECK_HIP(hipEventRecord(rev, im->comm));
       PG_CHECK_HIP(hipStreamWaitEvent(im->red, rev, 0));
-      PG_CHECK_HIP(hipStreamWaitEvent(im->red2, rev, 0));
       for (int g = 0; g < im->rings; ++g) {
         int t = pend_from;
         while (t < j) {
@@ -146,8 +171,7 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
             if (pg_kt_pair(im, &t0, &t1)) return -1;
             im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * (size_t)len * es);
           }
-          hipStream_t rs = (im->red_turn++ & 1) ? im->red2 : im->red;
-          if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, (size_t)len, dt, op, (void *)rs, t0, t1)) {
+          if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, (size_t)len, dt, op, (void *)im->red, t0, t1)) {
             pg_set_error("direct: %s", pgk_last_error());
             return -1;
           }

@@ -1,11 +1,9 @@
 /*
  * pg_exec.c -- executes a ring plan (pg_plan.c) on one rank.
  *
- * Streams per rank:
- *   comm       : transport groups (RCCL ncclSend/ncclRecv over xGMI), in plan order
- *   red, red2  : the reduce launches, alternating (every launch is independent
- *                of the previous one: other segments), so one launch's drain
- *                overlaps the next one's ramp
+ * Two HIP streams per rank:
+ *   comm : transport groups (RCCL ncclSend/ncclRecv over xGMI), in plan order
+ *   red  : the reduce launches
  * and two kinds of events:
  *   recv_ev[batch]  comm -> red : the batch's segments have landed
  *   red_ev[seg]     red -> comm : the segment's partial is reduced and may be
@@ -24,9 +22,11 @@
  * 71-73%.  Forwarding is not held up: a round's first sends need the previous
  * round's first launch only, which ran long before the round's last arrival.
  *
- * Every ordering between a reduce and anything else goes through the comm
- * stream (recv_ev before, red_ev after), never through the order of launches
- * on a reduce stream, which is what lets two of them alternate.
+ * One reduce stream on purpose.  Alternating the launches between two streams
+ * lets one launch's drain overlap the next one's ramp, which helps launches of
+ * 32 MiB per operand and less (+7 points of the HBM peak back to back) and
+ * costs 2-4 points at 128-256 MiB, the size the launches have here
+ * (tools/lab/split2_lab.hip, "whole calls alternating between two streams").
  *
  * Buffer reuse is safe by construction: a staging segment is overwritten by a
  * receive two rounds later, which the comm stream orders after the send of
@@ -143,7 +143,7 @@ static int pend_cmp(const void *pa, const void *pb) {
 }
 
 /* Reduce every pending step: the comm stream's position (behind the last
- * group that carried any of them) gates one of the two reduce streams, runs of
+ * group that carried any of them) gates the reduce stream, runs of
  * steps contiguous in both operands become one range each -- the segments of
  * one ring over consecutive batches are neighbours in the same block -- and
  * all ranges go out in one pgk_reduce_ranges launch (eight ranges at most per
@@ -151,7 +151,7 @@ static int pend_cmp(const void *pa, const void *pb) {
 static int reduce_pending(struct pg_impl *im, const struct pg_step *st, int npend, int nb, void *const bufs[5],
                           int dt, int op) {
   if (!npend) return 0;
-  hipStream_t rs = (im->red_turn++ & 1) ? im->red2 : im->red;
+  hipStream_t rs = im->red;
   hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
   PG_CHECK_HIP(hipEventRecord(rev, im->comm));
   PG_CHECK_HIP(hipStreamWaitEvent(rs, rev, 0));
@@ -269,10 +269,8 @@ int pg_exec_plan(struct pg_impl *im, const struct pg_step *st, int n,
     im->last_round_rec = cur_round;
     if (hook(im, hook_ctx, pg->world_size - 1)) return -1;   /* after the last round */
   }
-  /* join: the comm stream observes the last reduce of either stream */
+  /* join: the comm stream observes the last reduce */
   PG_CHECK_HIP(hipEventRecord(im->join_ev, im->red));
   PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join_ev, 0));
-  PG_CHECK_HIP(hipEventRecord(im->join2_ev, im->red2));
-  PG_CHECK_HIP(hipStreamWaitEvent(im->comm, im->join2_ev, 0));
   return 0;
 }

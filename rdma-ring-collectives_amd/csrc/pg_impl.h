@@ -62,11 +62,6 @@ struct pg_impl {
   void *xctx;                 /* ncclComm_t, or the virtual-rank context      */
 
   hipStream_t comm, red;      /* transfers / reductions                       */
-  hipStream_t red2;           /* second reduce stream: the ring executor and the direct exchange
-                                 alternate their (independent) reduce launches between red and
-                                 red2, so one launch's drain overlaps the next one's ramp       */
-  int red_turn;               /* which of the two the next launch takes        */
-  hipEvent_t join2_ev;        /* red2's counterpart of join_ev                 */
   size_t red_bytes;           /* PG_REDUCE_BYTES: arrived segments are reduced once this many
                                  bytes per operand are pending (or the round ends); 0 = per batch */
   int *pend; int pend_cap;    /* plan steps whose reduce is pending            */
@@ -115,6 +110,7 @@ int pg_default_transport(const struct pg *pg);            /* no PG_TRANSPORT: xg
 #define PG_ALGO_RING   0
 #define PG_ALGO_DIRECT 1
 int pg_direct_applies(const struct pg *pg, int count);
+int pg_direct_prepare(struct pg *pg, int count, int dt);  /* 1 go, 0 every rank takes the ring, -1 failed */
 int pg_direct_reduce_scatter(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);
 int pg_direct_all_gather(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt);
 int pg_direct_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, int dt, int op);

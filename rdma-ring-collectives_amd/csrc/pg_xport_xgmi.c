@@ -343,8 +343,9 @@ static int cmp_double(const void *a, const void *b) {
 static int choose_mode(struct pg *pg) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   struct xgmi_ctx *x = ctx_of(pg);
-  /* two passes, the better rate of each direction: a one-off stall in one pass
-   * (another process's work on the links or the GPU) does not decide the mode */
+  /* two passes, the better rate of each direction.  A precaution, not a
+   * response to an observed failure: the choice is made once per handle from
+   * about a millisecond of traffic, and a second pass costs as little. */
   double g[4] = {0, 0, 0, 0}, best[2] = {0, 0};
   for (int pass = 0; pass < 2; ++pass) {
     if (pgx_xgmi_link_probe(pg, XG_PROBE_BYTES, 3, g)) return -1;

@@ -60,6 +60,8 @@ class PgStats(ctypes.Structure):
         ("sync_us", ctypes.c_double), ("copy_us", ctypes.c_double), ("barrier_us", ctypes.c_double),
         ("kernel_us", ctypes.c_double), ("zero_copy", ctypes.c_int32), ("retried", ctypes.c_int32),
         ("calls_redone", ctypes.c_int64), ("red_kernel_us", ctypes.c_double), ("red_kernel_bytes", ctypes.c_int64),
+        ("transport", ctypes.c_int32), ("algo_direct", ctypes.c_int32), ("xgmi_push", ctypes.c_int32),
+        ("xgmi_mode_auto", ctypes.c_int32), ("probe_read_gbs", ctypes.c_double), ("probe_write_gbs", ctypes.c_double),
     ]
 
 

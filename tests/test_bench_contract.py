@@ -86,3 +86,95 @@ def test_batch_launch_at_defaults_above_70_percent():
     first = ks["ring_batches"]["rows"][0]
     assert first[:3] == [4 << 20, 4, 2]
     assert first[5] >= 0.70 and first[7] >= 0.70
+
+
+# ---- round 3: the same contract on this round's lines, plus what round 3 added --------------------------
+
+def test_r03_bench_line_contract():
+    line = _line("r03_bench.json")
+    base = json.loads((ROOT / "BASELINE.json").read_text())
+    for k in REQUIRED + ("elapsed_s", "time_budget_s"):
+        assert k in line, k
+    assert line["metric"] == base["metric"] and line["n_gpus"] == 1 and line["vs_baseline"] is None
+    r = line["roofline"]
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-4) and r["peak"] == 8000.0
+    assert r["achieved"] == pytest.approx(r["bytes_per_launch"] / (r["kernel_mean_ms"] * 1e-3) / 1e9, rel=1e-3)
+    pmc = json.loads((PROF / "pmc_traffic.json").read_text())["reduce_f64_sum_256MiB"]["hbm_bytes_per_launch"]
+    assert r["traffic"] == pytest.approx(pmc, rel=1e-4) and 0.99 < r["traffic"] / r["bytes_per_launch"] < 1.05
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] in ("reference", "port") and cpu["cores"] >= 1 and cpu["value"] > 0 and cpu["sample"]
+    # every leg is clocked and the whole run fits the budget it was given
+    el = line["elapsed_s"]
+    assert {"kernel_sizes", "kernel_leg", "cpu_baseline", "total"} <= set(el)
+    assert el["total"] <= line["time_budget_s"]
+
+
+def test_r03_executor_launch_at_defaults():
+    """The reduce launch the ring executor makes at the library defaults
+    (PG_REDUCE_BYTES = 128 MiB pending over two rings, one pgk_reduce_ranges
+    launch) reaches 78% of the HBM peak kernel-stamped; the single transport
+    group it replaced (4 MiB x 4 x 2 rings) is kept beside it."""
+    ks = _line("r03_bench.json")["kernel_sizes"]
+    cols = ks["ring_batches"]["columns"]
+    first, group = ks["ring_batches"]["rows"][0], ks["ring_batches"]["rows"][1]
+    assert first[cols.index("bytes_per_operand")] == 128 << 20 and first[cols.index("rings")] == 2
+    assert first[cols.index("stamped_frac")] >= 0.78 and first[cols.index("frac")] >= 0.78
+    assert group[cols.index("bytes_per_operand")] == 32 << 20
+    assert first[cols.index("frac")] > group[cols.index("frac")]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_r03_rehearsal_lines_checked_out(world):
+    line = _line(f"r03_bench_n{world}_onegpu_rehearsal.json")
+    assert line["n_gpus"] == world and line["metric"] == _line("r03_bench.json")["metric"]
+    assert line["elapsed_s"]["total"] <= line["time_budget_s"]
+    ring = line["ring"]
+    assert {"xgmi", "rccl"} <= set(ring)
+    legs = [v for v in ring.values() if isinstance(v, dict) and "skipped" not in v]
+    assert legs and all(v.get("ok") is True for v in legs)
+    for name, v in ring.items():
+        if not isinstance(v, dict) or "skipped" in v:
+            continue
+        assert f"ring.{name}" in line["elapsed_s"]
+        phases = v["last_call_phases"]
+        assert phases["redone"] is False and phases["calls_redone_total"] == 0
+        # the library itself names the data path that ran
+        assert phases["path"]["transport"] == ("xgmi" if name.startswith("xgmi") else "rccl")
+        assert v["in_ring_reduce"]["launches_per_rank"] >= 1
+        for key in ("config5_prod_mixed", "eager_4KiB", "rccl_native", "host_buffers"):
+            part = v.get(key)
+            if part is None or (isinstance(part, dict) and "skipped" in part):
+                continue
+            if key == "config5_prod_mixed":
+                assert all(row["ok"] is True for row in part)
+            elif key == "eager_4KiB":
+                assert part["reduce_scatter"]["ok"] and part["all_reduce"]["ok"]
+            elif key == "host_buffers":
+                assert part["ok"] is True
+            else:
+                assert part["i32_sum_bit_exact"] and part["f64_sum_within_tol"]
+                assert part["i32_prod_bit_exact"] and part["f64_prod_within_tol"]
+                assert part["i32_all_reduce_bit_exact"] and part["i32_all_gather_bit_exact"]
+
+
+@pytest.mark.parametrize("world,key,knob", [(4, "chunk_sweep", "chunk_bytes"), (8, "inflight_sweep", "inflight")])
+def test_r03_sweeps_cover_both_schedules(world, key, knob):
+    """BASELINE configs 3 and 4 name a ring with a PG_CHUNK_BYTES / PG_INFLIGHT
+    sweep: every committed sweep row names its schedule (`algo`), both the W-1
+    round ring and the direct exchange are swept over every value, and each row
+    carries the roofline fraction of the reduce launches inside it.  A row
+    without `algo` fails here."""
+    sw = _line(f"r03_bench_n{world}_onegpu_rehearsal.json")["ring"]["rccl"][key]
+    cols = sw["columns"]
+    assert cols[:5] == ["size", "rounds", "inflight", "time_us", "GB/s"]     # reference README.md:85
+    for need in ("chunk_bytes", "is_default", "algo", "in_ring_reduce_frac"):
+        assert need in cols, need
+    a, k, f = cols.index("algo"), cols.index(knob), cols.index("in_ring_reduce_frac")
+    for row in sw["rows"]:
+        assert len(row) == len(cols) and row[a] in ("ring", "direct"), row
+        assert 0.0 < row[f] <= 1.0, row
+    values = {1 << e for e in range(16, 29)} if knob == "chunk_bytes" else {1, 2, 4, 8, 16}
+    for algo in ("ring", "direct"):
+        assert {row[k] for row in sw["rows"] if row[a] == algo} == values, algo
+        assert sum(row[cols.index("is_default")] for row in sw["rows"] if row[a] == algo) == 1
+    assert set(sw["by_algo"]) == {"ring", "direct"} and sw["truncated_by_time_budget"] is False

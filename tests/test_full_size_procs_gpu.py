@@ -18,7 +18,15 @@ b: x[b+d] op x[b+2d] op ... op x[b]), one IEEE operation per element and step,
 as tests/test_full_size_gpu.py does for the ring executor.  Every rank makes
 every rank's input from a counter-based formula of (rank, index), so no input
 crosses processes except through the transport.  The doubles carry full
-53-bit mantissas, so a different fold order would change their bits."""
+53-bit mantissas, so a different fold order would change their bits.
+
+That GPU-side expectation is itself a restatement, so it is pinned to the C
+oracle where the oracle is affordable: for every checked block, windows at the
+start and the end of every ring part (the part boundaries included) are folded
+on the host by the oracle's own reduce loop (orc_reduce_inplace, the
+restatement of reference src/pg.c:151-159) in the ring order orc_ring_step
+gives, from inputs regenerated for just those windows, and compared with the
+transport's output bit for bit."""
 import os
 import pathlib
 import socket
@@ -81,6 +89,41 @@ def _expected(torch, world, rank, count, dt, op, rings, ring_step, block_range):
     return out
 
 
+WINDOW = 1 << 15         # elements per oracle-checked window
+
+
+def _oracle_windows(ln, rings):
+    """(lo, hi, ring part) windows of a block of ln elements: the first and the
+    last WINDOW elements of every ring part."""
+    wins = []
+    for g in range(rings):
+        lo, hi = -(-g * ln // rings), -(-(g + 1) * ln // rings)
+        if lo == hi:
+            continue
+        wins.append((lo, min(hi, lo + WINDOW), g))
+        if hi - lo > WINDOW:
+            wins.append((hi - WINDOW, hi, g))
+    return wins
+
+
+def _oracle_check(torch, orc, got_block, world, b, boff, bln, dt, op, rings):
+    """Windows of block b of the transport's output against the C oracle's fold
+    of the same windows of every rank's input.  Returns the windows that differ."""
+    tdt = torch.int32 if dt == 0 else torch.float64
+    bad = []
+    for lo, hi, g in _oracle_windows(bln, rings):
+        d = orc.ring_step(world, rings, g) % world
+        win = torch.empty(hi - lo, dtype=tdt, device="cuda")
+        acc = None
+        for j in range(1, world + 1):                  # x[b+d] op x[b+2d] op ... op x[b]
+            _fill(torch, win, (b + j * d) % world, boff + lo, dt, op)
+            xq = win.cpu().numpy()
+            acc = xq.copy() if acc is None else orc.reduce(acc, xq, dt, op)
+        if got_block[lo:hi].cpu().numpy().tobytes() != acc.tobytes():
+            bad.append((lo, hi, g))
+    return bad
+
+
 def _env(transport, rank, port, mode=None, algo=None):
     env = dict(PG_TRANSPORT=transport, PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
                PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="120000", PG_XGMI_MODE=mode, PG_ALGO=algo)
@@ -130,6 +173,9 @@ def _worker(rank, world, port, q, calls, transport, mode, algo):
                 boff, bln = pgamd.block_range(count, world, b)
                 want = _expected(torch, world, b, count, dt, op, rings, orc.ring_step, pgamd.block_range)
                 got = out[:bln] if coll == "rs" else out[boff:boff + bln]
+                bad_windows = _oracle_check(torch, orc, got, world, b, boff, bln, dt, op, rings)
+                if bad_windows:
+                    fails.append((i, coll, dt, op, count, b, "differs from the C oracle in windows", bad_windows))
                 if dt == 1:                          # bits, not values (-0.0 == 0.0)
                     got, want = got.view(torch.int64), want.view(torch.int64)
                 if not torch.equal(got, want):

@@ -56,9 +56,10 @@ def _rccl_env(rank, port, split_hosts):
     return env
 
 
-def _worker(rank, world, port, q, rings, chunk_bytes, inflight, cases, algo):
+def _worker(rank, world, port, q, rings, chunk_bytes, inflight, cases, algo, env_extra=None):
     os.environ.update(_rccl_env(rank, port, True), PG_RINGS=str(rings), PG_CHUNK_BYTES=str(chunk_bytes),
                       PG_INFLIGHT=str(inflight))
+    os.environ.update(env_extra or {})
     if algo:
         os.environ["PG_ALGO"] = algo
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
@@ -358,4 +359,34 @@ def test_forced_xgmi_without_reach_fails_on_every_rank(gpu):
     for rank, out in results:
         assert out.get("rc") == -1, (rank, out)
         assert "cannot map a peer" in out["err"], (rank, out)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_direct_exchange_falls_back_to_ring_when_its_gather_area_cannot_grow(gpu, tmp_path):
+    """The direct exchange's gather area is as large as the whole input.  When
+    one rank cannot allocate it (test hook PG_TEST_FAIL_STAGE_ALLOC), every rank
+    runs that call on the ring instead: same bits, nobody hangs, and later calls
+    agree again on whether the area has to grow."""
+    cases = [("rs", 1, 0, 300001, True, False), ("ar", 0, 1, 524288, True, False), ("rs", 1, 0, (1 << 20) + 3, True, False),
+             ("ar", 1, 0, 100003, False, False), ("rs", 0, 0, 4099, True, False)]
+    prefix = str(tmp_path / "trace")
+    results, procs = _run(3, _worker, lambda r: (2, 1 << 18, 2, cases, "direct",
+                                                 {"PG_TEST_FAIL_STAGE_ALLOC": "1", "PG_TRACE_FILE": prefix}))
+    for rank, fails in results:
+        assert not fails, (rank, fails)
+    assert all(p.exitcode == 0 for p in procs)
+    traces = "".join(f.read_text() for f in tmp_path.glob("trace.*"))
+    assert traces.count("falling back to the ring") >= 3 * 4      # 3 ranks x the 4 calls above eager size
+
+
+@pytest.mark.parametrize("algo,red_bytes", [("ring", 0), ("ring", 1 << 18), ("direct", 0), ("direct", 3 << 17)])
+def test_rccl_reduce_launch_sizes(gpu, algo, red_bytes):
+    """PG_REDUCE_BYTES over RCCL with real processes: 64 KiB segments, 2 in
+    flight, 3 ranks, two rings; the arrived segments are reduced per group (0)
+    or once a few groups are pending, host and device buffers, in place: the
+    oracle ring's bits either way."""
+    cases = [c for c in CASES if c[3] != 1 << 20]
+    results, procs = _run(3, _worker, lambda r: (2, 1 << 16, 2, cases, algo, {"PG_REDUCE_BYTES": str(red_bytes)}))
+    for rank, fails in results:
+        assert not fails, (rank, fails)
     assert all(p.exitcode == 0 for p in procs)

@@ -27,7 +27,14 @@ extern "C" int split2_run(void* fn, char* base, size_t pair_stride, int pairs, s
   const size_t h = (n / 2 + 2047) / 2048 * 2048;      // halves on a 16 KiB boundary
   int rc = 0, k = 0;
   for (int i = 0; i < warm + reps && !rc; ++i) {
-    if (i == warm) hipEventRecord(t0, A);
+    if (i == warm) {
+      // the timed region starts with both streams idle and B held behind t0: a
+      // stream that ran ahead through the warm-up must not start timed work early
+      hipStreamSynchronize(A);
+      hipStreamSynchronize(B);
+      hipEventRecord(t0, A);
+      hipStreamWaitEvent(B, t0, 0);
+    }
     char* d = base + pair_stride * (size_t)(k++ % pairs);
     char* s = d + pair_stride / 2;
     switch (mode) {
