@@ -510,17 +510,21 @@ void launch_ranges_nt(int block, int unroll, unsigned grid, const RangeList<T>& 
 }
 
 // k ranges, each 16-B congruent (plan_for(...).vec), in one launch; the
-// shape is the one a single launch of the largest range would use, and each
-// range gets the blocks that launch would give it.  Returns hipErrorInvalidValue
-// (nothing launched) when the ranges do not fit one grid.
+// shape is the one a single launch of all the ranges' bytes would use (a launch
+// of R ranges streams like one launch of their sum: 2 x 64 MiB runs at 81.6%
+// of the HBM peak with the 128 MiB shape, 80.7% with the 64 MiB one, and
+// 2 x 128 MiB at 82.2% against 80.6%, kernel-stamped,
+// tools/lab/ranges_shape_probe.py), and each range gets the blocks that shape
+// gives it.  Returns hipErrorInvalidValue (nothing launched) when the ranges do
+// not fit one grid.
 template <typename T, int OP>
 hipError_t launch_ranges_t(T* const* outs, const T* const* as, const T* const* bs, const size_t* ns, int k,
                            hipStream_t s, Timing tm) {
   RangeList<T> rl{};
-  size_t most = 0;
-  for (int j = 0; j < k; ++j) most = ns[j] > most ? ns[j] : most;
+  size_t sum = 0;
+  for (int j = 0; j < k; ++j) sum += ns[j];
   int block = 0, unroll = 0;
-  shape_for(most * sizeof(T), &block, &unroll);
+  shape_for(sum * sizeof(T), &block, &unroll);
   const size_t tile = (size_t)block * (size_t)unroll, W = 16 / sizeof(T);
   size_t total = 0;
   rl.k = k;

@@ -111,3 +111,42 @@ def test_staged_exact_capacity_and_free_memory(gpu, lib, oracle):
     free1, _ = torch.cuda.mem_get_info()
     assert free1 == free0
     assert to_host(torch, R).tobytes() == xs[0].tobytes()
+
+
+def test_staged_all_reduce_captured_in_hip_graph(gpu, lib, oracle):
+    """What the entry point is for: captured into a hipGraph (torch.cuda.CUDAGraph
+    is hipGraph on ROCm; only kernel launches are recorded, no memset nodes) and
+    replayed.  The graph holds an in-place all-reduce of four buffers; every
+    replay must equal the eager call on the same inputs, with eager calls of the
+    same entry point (other sizes, so the shared array holds other contents) and
+    synchronisations between the replays."""
+    torch = gpu
+    world, count, dt, op, rings = 4, 50001, 1, 0, 2
+    xs = [oracle.fill(count, dt, op, 31000 + r) for r in range(world)]
+    bufs = [to_dev(torch, x) for x in xs]
+    ps = (ctypes.c_void_p * world)(*[ptr(b) for b in bufs])
+    assert lib.pgk_all_reduce_staged(None, None, world, 0, rings, dt, op, None) == 0     # set-up, outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            sh = torch.cuda.current_stream().cuda_stream
+            assert lib.pgk_all_reduce_staged(ps, ps, world, count, rings, dt, op, sh) == 0
+    state = [x.copy() for x in xs]
+    for rep in range(4):
+        for b, v in zip(bufs, state):                 # this replay's inputs
+            b.copy_(torch.from_numpy(v))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        want = oracle.ring_all_reduce(state, dt, op, rings)
+        for r in range(world):
+            assert to_host(torch, bufs[r]).tobytes() == want[r].tobytes(), (rep, r)
+        # eager work of the program's own between the replays, on the same shared array
+        small = [oracle.fill(777 + rep, 0, 1, 32000 + 5 * rep + r) for r in range(3)]
+        got = _staged(lib, torch, small, 777 + rep, 0, 1, 1, False)
+        ref = oracle.ring_all_reduce(small, 0, 1, 1)
+        for r in range(3):
+            assert got[r].tobytes() == ref[r].tobytes(), (rep, r, "eager between replays")
+        state = [oracle.fill(count, dt, op, 33000 + 10 * rep + r) for r in range(world)]
