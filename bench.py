@@ -179,7 +179,7 @@ def kernel_leg(lib, args, rank, world):
     launch stream, / K), and kernel-stamped per-launch durations from an
     untimed cross-check pass."""
     # one allocation carved into N_PAIRS adjacent (dst, src) pairs, as the size
-    # table does: operand placement moves this kernel by 1-5 % (DESIGN.md §4,
+    # table does: operand placement moves this kernel by 1-5 % (measured:
     # "placement"), and separate torch allocations land wherever the caching
     # allocator puts them, so the primary figure would depend on what ran before
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
@@ -296,7 +296,7 @@ def size_leg(lib, rank, world, reps=20):
                          size, round(ms * 1e3, 2), round(gbs, 1), round(gbs / HBM_PEAK_GBS, 4),
                          round(sms * 1e3, 2), round(sgbs / HBM_PEAK_GBS, 4)])
     # the per-launch edge: least-squares t = t0 + traffic / bw over the f64-sum rows >= 16 MiB
-    # (DESIGN.md §4: a fixed ramp + drain per launch against a streaming rate)
+    # (a fixed ramp + drain per launch against a streaming rate)
     fit = {}
     for col, key in ((3, "events"), (6, "stamped")):
         pts = [(3 * r_[2], r_[col]) for r_ in rows if r_[0] == "f64" and r_[1] == "sum" and r_[2] >= (16 << 20)]
@@ -454,7 +454,7 @@ def cpu_baseline(args):
             pass
     del d, s
     concurrent = None
-    if args.cpu_procs > 1:       # W ranks of the reference at once (SURVEY §8d), in a fresh child process
+    if args.cpu_procs > 1:       # W ranks of the reference at once, in a fresh child process
         import subprocess
         try:
             r = subprocess.run([sys.executable, "-m", "oracle.cpu_concurrent", "--procs", str(args.cpu_procs),
@@ -503,7 +503,7 @@ def config1_leg(lib):
     """BASELINE config 1 (2-rank ring, int32 sum, count 1,048,576): each rank
     reduces one 2 MiB block (524,288 elements).  CPU: the reference's own
     pg_reduce_scatter(W=2, R=0, chunk 2 MiB), which is exactly that one
-    reduce_inplace (SURVEY.md §8d).  GPU: pgk_reduce on the same block, kernel
+    reduce_inplace.  GPU: pgk_reduce on the same block, kernel
     time and host-call wall time."""
     import statistics
     from oracle.pyoracle import Oracle, Reference
@@ -612,7 +612,7 @@ def _nccl_group():
 
 
 def native_crosscheck(lib, h, rank, world, x_full, dt_full):
-    """pg_reduce_scatter against RCCL's own reduce-scatter (SURVEY §8e).
+    """pg_reduce_scatter against RCCL's own reduce-scatter.
 
     Random inputs, 16 Mi elements per rank (a multiple of W, so both libraries
     use the same uniform blocks): full-range int32 for sum and product, U[-1,1)
@@ -937,8 +937,8 @@ def ring_leg(lib, args, rank, world, transport, sink):
         sink[transport] = res          # visible to the watchdog's print while the leg runs
         # every leg reads the SAME input allocation: a fresh tensor after the
         # previous leg's empty_cache() lands at the freed address under a new HIP
-        # buffer id, and the xgmi transport never exports such a range (DESIGN.md
-        # §5a, "Reused addresses"): the forced-mode legs would then time the slot
+        # buffer id, and the xgmi transport never exports such a range (an importer may
+        # still hold a mapping of the freed one): the forced-mode legs would then time the slot
         # copy instead of the zero-copy read they are there to compare
         x = _LEG_INPUT.get((count, dt))
         if x is None:
@@ -988,8 +988,8 @@ def ring_leg(lib, args, rank, world, transport, sink):
         # the direct exchange (this handle, the default on one node) and the W-1
         # round ring (PG_ALGO=ring, two counter-rotating rings, a second handle).
         # Every row names its schedule and carries the roofline fraction of the
-        # reduce launches inside it.  DESIGN.md states the rule that turns these
-        # rows into the next defaults.
+        # reduce launches inside it; by_algo names each schedule's fastest row and
+        # its gain over that schedule's default row.
         sweep = None
         if transport == "rccl" and world == 4:
             sweep = ("chunk_bytes", [1 << e for e in range(16, 29)], "chunk_sweep", 5)   # 64 KiB .. 256 MiB

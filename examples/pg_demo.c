@@ -1,7 +1,7 @@
 /*
  * examples/pg_demo.c -- a plain C caller of the reference API (include/pg.h),
  * built exactly as a user of the reference would build theirs, but linked
- * against libpg_amd.so (INTEGRATION.md §1):
+ * against libpg_amd.so:
  *
  *   gcc -O2 -Iinclude examples/pg_demo.c -Lrdma-ring-collectives_amd -lpg_amd \
  *       -Wl,-rpath,$PWD/rdma-ring-collectives_amd -o pg_demo

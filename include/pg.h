@@ -7,7 +7,7 @@
  * existing harness can still read rank/world_size and set chunk_bytes /
  * eager_max / inflight directly (reference pg.h:40-46).
  *
- * What changed underneath (see DESIGN.md):
+ * What changed underneath:
  *   - one process per GPU; the ring hop is RCCL point-to-point over xGMI
  *     instead of RC queue pairs (reference src/RDMA_api.c, src/pg_net.c);
  *   - every arriving segment is reduced by a hand-written gfx950 HIP kernel

@@ -156,8 +156,8 @@ PG_API int pgx_sim_run(int world, int coll, void *const *sendbufs, void *const *
  * reading and writing at once.  Otherwise staged through HBM in chunk_bytes
  * pieces (0 = 16 MiB) that flow through 3 device slots: uploads (dst, src)
  * and the reduce run on the calling thread while a helper thread downloads
- * finished pieces.  Synchronous.  This is what the PCIe-inclusive rate in
- * DESIGN.md measures. */
+ * finished pieces.  Synchronous.  This call is what the PCIe-inclusive rate
+ * of the hot path is measured on. */
 PG_API int pgx_reduce_host(void *dst, const void *src, size_t n, int datatype, int op, size_t chunk_bytes);
 
 /* Measurements of the last collective on this handle. */

@@ -117,7 +117,7 @@ PG_API int pgk_synchronize(void);
 /* Launch tuning, process-wide.  blocks_per_cu: grid cap = CUs x blocks_per_cu
  * (0 = uncapped one-shot grid, <0 = keep).  nontemporal: 1 = nt loads/stores,
  * 0 = default cache policy, <0 = keep.  Defaults are the measured best
- * (DESIGN.md). */
+ * on MI355X. */
 PG_API int pgk_tune(int blocks_per_cu, int nontemporal);
 
 /* Vector-kernel shape: threads per block x 16-byte vectors per operand each

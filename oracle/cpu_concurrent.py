@@ -1,6 +1,6 @@
 """TEST INFRASTRUCTURE ONLY -- the CPU baseline with W concurrent ranks.
 
-SURVEY.md §8(d): besides the 1-core figure, time W processes at once, each
+Besides the 1-core figure, time W processes at once, each
 pinned to its own host core and each running the reference's reduce loop
 (oracle/_ref, src/pg.c:151-159) over its own 256 MiB double chunk -- what W
 CPU ranks of the reference would sustain on this host.  Started by bench.py's

@@ -141,8 +141,8 @@ void orc_ring_block(size_t count, int world, int b, size_t *off_elems, size_t *l
  * +1, -1, then +3, -3, +5, ... kept when coprime with world and not yet used
  * mod world; when they run out the list repeats.  Ring 0 (+1) is the
  * reference's ring (README.md:68-71, rs_{send,recv}_chunk_index at
- * src/pg.c:141-148); the further rings are this build's extension (SURVEY.md
- * §8f "multi-ring"), restated here independently of the library's code. */
+ * src/pg.c:141-148); the further rings are this build's extension (rings over
+ * further xGMI links), restated here independently of the library's code. */
 int orc_ring_step(int world, int rings, int g) {
     int offs[4] = {1, -1}, m = 2;
     for (int c = 3; m < 4 && c < 2 * world; c += 2) {

@@ -3,8 +3,8 @@
  *
  * Appended after the reference's extracted path lines (see ref_prelude.h).
  * Exposes the reference's static helpers and its collectives, driven with a
- * hand-filled struct pg {rank, world_size, chunk_bytes} exactly as SURVEY.md
- * Appendix A prescribes, under ref_* names for ctypes.
+ * hand-filled struct pg {rank, world_size, chunk_bytes} (no connect_process_group,
+ * which needs libibverbs), under ref_* names for ctypes.
  */
 #include <time.h>
 

@@ -109,7 +109,7 @@ int pg_stream_wait(hipStream_t s) {
 }
 
 /* Device buffers: the caller's producers are the work it enqueued on the null
- * stream before the call ("Device buffers"; work on other
+ * stream before the call (work on other
  * streams the caller orders before the call itself).  The collective must not
  * read its buffers before that work ends.
  * An idle null stream (the usual case: the caller synchronised, or produced
@@ -341,7 +341,7 @@ static void pg_defaults(struct pg *pg) {
  * (every entry of the server list names the same host) and W <= 16 -- it is
  * the one exercised with real processes (tests/test_xgmi_gpu.py) and it pulls
  * over all of a GPU's links at once -- else the RCCL ring, which also crosses
- * nodes.  Both give the same bits (ring fold order). */
+ * nodes.  Both give the same bits (every transport folds in the ring's order). */
 int pg_default_transport(const struct pg *pg) {
   if (pg->world_size > 16) return PG_TRANSPORT_RCCL;
   for (int i = 1; i < pg->world_size; ++i)

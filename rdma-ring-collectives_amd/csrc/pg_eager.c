@@ -1,5 +1,5 @@
 /*
- * pg_eager.c -- one-shot exchange for small messages (eager).
+ * pg_eager.c -- one-shot exchange for small messages (the eager path).
  *
  * The reference declares an eager threshold (eager_max, src/constants.h:75,
  * pg.h:44) but its ring always runs W-1 rounds (src/pg.c:277-289,
@@ -17,7 +17,7 @@
  *
  * Fold order = the ring's (part g of block b: x[b+d] op x[b+2d] op ... op x[b]
  * with d = pg_ring_offset(W, rings, g): +1, -1, +3, -3; see
- * pg_plan.c, include/pg_ext.h and DESIGN.md §2), so results are bit-identical
+ * pg_plan.c and include/pg_ext.h), so results are bit-identical
  * to the ring path for int32 and double alike.  Used by the point-to-point transports (RCCL,
  * in-process threads) for W <= 16; xgmi has its own direct-read one-shot.
  * PG_EAGER_ONESHOT=0 turns it off.

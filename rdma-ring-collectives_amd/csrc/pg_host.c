@@ -1,7 +1,7 @@
 /*
  * pg_host.c -- the chunk reduce with both operands in host memory
  * (pgx_reduce_host, include/pg_ext.h): the PCIe-inclusive form of the hot path
- * that DESIGN.md §8 reports beside the device-resident rate.  Pinned, mapped
+ * that is reported beside the device-resident rate.  Pinned, mapped
  * operands are reduced in place by one kernel over PCIe; pageable ones flow
  * through HBM slots.
  */

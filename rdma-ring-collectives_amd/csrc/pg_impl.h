@@ -1,7 +1,8 @@
 /*
  * pg_impl.h -- internals of libpg_amd.so (not installed).
  *
- * Layering (mirrors the reference's L3/L2/L1 split):
+ * Layering (mirrors the reference's split into collectives / group lifecycle / bootstrap,
+ * src/pg.c:264-339 / :185-262 / src/pg_net.c):
  *   pg.c          public API, validation, host<->HBM staging, loopback mock
  *   pg_plan.c     ring schedule as data (pure C, no HIP)
  *   pg_exec.c     executes a plan: transport groups on the comm stream,

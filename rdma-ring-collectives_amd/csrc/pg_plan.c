@@ -9,7 +9,7 @@
  * the schedule can be checked without a GPU (tests/test_plan_gloo.py runs it
  * over two gloo processes).
  *
- * Differences from the reference mock, all deliberate (DESIGN.md §Semantics):
+ * Differences from the reference mock, all deliberate:
  *   - the ring partition unit is the block ceil(count/W), not chunk_bytes;
  *     chunk_bytes is the pipelining segment inside a block (README.md:17,75);
  *   - the index functions are evaluated at rank-1 so rank r ends with block r
@@ -19,9 +19,9 @@
  *     src/pg.c:282-287);
  *   - with rings = 2 (default) the second half of every block runs the mirror
  *     schedule in the other direction, so both directions of each link carry
- *     data (SURVEY.md §8f "bidirectional ring"); rings = 3, 4 add rings of
+ *     data (a bidirectional ring); rings = 3, 4 add rings of
  *     step +3 / -3 (world permitting: pg_ring_offset), each over its own pair
- *     of xGMI links (§8f "multi-ring"); the reference's README describes one
+ *     of xGMI links (multi-ring); the reference's README describes one
  *     ring (README.md:68-71).
  */
 #include <stddef.h>

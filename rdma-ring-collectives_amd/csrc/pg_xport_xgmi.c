@@ -9,7 +9,7 @@
  * -- and fold them in the exact order the ring would:
  *     out = x[r+1] op x[r+2] op ... op x[r]        (indices mod W)
  * which is bit-identical to the RCCL ring and to the oracle's ring simulator.
- * This is the "fused receive-reduce" + "multi-link" rows of SURVEY.md §8f.
+ * This is a fused receive-reduce over every link of the GPU at once.
  *
  * Memory: each rank owns up to two IPC-exportable HBM regions, each mapped
  * into every peer with hipIpcOpenMemHandle and double-buffered by call parity:
@@ -56,7 +56,7 @@ struct xg_import {
 /* A cached mapping of a peer's input keeps that allocation's HBM alive in the
  * peer even after it frees it.  Mappings of allocations at least this large
  * are kept only while they are the peer's current input: the first call with
- * another input closes them (ADVICE r01; tests/test_xgmi_gpu.py::
+ * another input closes them (tests/test_xgmi_gpu.py::
  * test_xgmi_freed_large_input_is_released).  Small ones stay in the LRU. */
 #define XG_KEEP_MAX (256ull << 20)
 
@@ -1007,7 +1007,7 @@ int pg_xgmi_all_reduce(struct pg *pg, void *sendbuf, void *recvbuf, int count, i
 }
 
 /* ---- link probe ----------------------------------------------------------------
- * Measures what the transport's traffic rides on ("measure
+ * Measures what the transport's traffic rides on (the rule followed: "measure
  * the unidirectional per-link rate with a P2P probe before quoting roofline for
  * the ring").  Every rank runs the same four phases, each `reps` copy launches
  * of `bytes` (pgk_gather) timed with HIP events, with barriers in between:

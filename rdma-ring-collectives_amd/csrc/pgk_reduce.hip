@@ -316,7 +316,7 @@ void set_err(const char* fmt, ...) {
   va_end(ap);
 }
 
-// Tuning (process-wide).  Measured on MI355X: see DESIGN.md "Kernel tuning".
+// Tuning (process-wide).  The defaults are the measured best on MI355X (the figures are beside each knob).
 int g_blocks_per_cu = 0;   // one-shot grid: 6403 vs 6200 GB/s capped at 8/CU (sweep r01)
 int g_nontemporal = 1;
 // Vector shape: 0x0 = by size (shape_for); else forced by pgk_tune_shape.

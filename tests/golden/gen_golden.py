@@ -8,11 +8,11 @@ built by `make -C oracle`):
 Every expected output below comes from the reference's src/pg.c (lines 104-179
 and 264-339 compiled unchanged by oracle/Makefile) -- reduce_inplace exposed
 through ref_reduce_inplace, and pg_reduce_scatter / pg_all_gather /
-pg_all_reduce driven with a hand-filled struct pg (SURVEY.md Appendix A).
-Inputs come from the splitmix64 generator of SURVEY.md §8d (orc_fill); the
+pg_all_reduce driven with a hand-filled struct pg.
+Inputs come from the splitmix64 generator (orc_fill); the
 stored digests let a test regenerate the large inputs and check them.
 Only in-bounds shapes are generated (the reference reads/writes past its
-buffers for some shapes: SURVEY.md §0.5).
+buffers for some shapes).
 """
 from __future__ import annotations
 
@@ -97,7 +97,7 @@ def main() -> None:
             key = f"sp{dt}{op}"
             arrays[key + "_dst0"], arrays[key + "_src"], arrays[key + "_out"] = d0, s, out
             manifest["specials"].append({"key": key, "dt": dt, "op": op, "n": int(d0.size)})
-    # known answers quoted in SURVEY.md §8c must hold
+    # known answers (worked by hand from reference src/pg.c:151-159, :264-291) must hold
     assert ref.reduce(np.array([2**31 - 1], np.int32), np.array([2**31 - 1], np.int32), 0, 0)[0] == -2
     assert ref.reduce(np.array([65536], np.int32), np.array([65536], np.int32), 0, 1)[0] == 0
     assert ref.reduce(np.array([-123456789], np.int32), np.array([987654], np.int32), 0, 1)[0] == 1530050434

@@ -73,7 +73,7 @@ def test_connect_process_group_single_host(gpu, lib, monkeypatch):
     assert lib.pg_all_reduce(ptr(X), ptr(Y), 10, 1, 0, h) == 0
     assert to_host(torch, Y).tobytes() == x.tobytes()
     assert lib.pg_close(h) == 0
-    # env precedence: PG_CHUNK_BYTES wins over the default (reference bug)
+    # env precedence: PG_CHUNK_BYTES wins over the default (reference bug: src/pg.c:203-209 sets the defaults before :42-50 reads the env)
     monkeypatch.setenv("PG_CHUNK_BYTES", "65536")
     monkeypatch.setenv("PG_INFLIGHT", "7")
     assert lib.connect_process_group(socket.gethostname().encode(), ctypes.byref(h)) == 0

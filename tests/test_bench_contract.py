@@ -59,7 +59,7 @@ def test_rehearsal_lines_checked_out(world):
     legs = [v for v in ring.values() if isinstance(v, dict)]
     assert legs and all(v.get("ok") is True for v in legs)
     assert all(v.get("host_buffers_ok", True) is True for v in legs)
-    # round 2: every transport ran, the RCCL ring included, and nothing was redone
+    # every transport ran, the RCCL ring included, and nothing was redone
     assert {"xgmi", "rccl"} <= set(ring)
     for v in legs:
         for row in v.get("config5_prod_mixed", []):
@@ -80,7 +80,7 @@ def test_rehearsal_lines_checked_out(world):
 def test_batch_launch_at_defaults_above_70_percent():
     """The executor's reduce launch at the library defaults (4 MiB x 4
     inflight x 2 rings, one pgk_reduce_ranges launch) keeps >= 70% of the HBM
-    peak (VERDICT r01 item 2), and the size table starts at the in-ring sizes."""
+    peak, and the size table starts at the in-ring sizes."""
     ks = _line("r02_bench.json")["kernel_sizes"]
     assert {r[2] for r in ks["rows"]} >= {4 << 20, 16 << 20, 32 << 20, 64 << 20}
     first = ks["ring_batches"]["rows"][0]
@@ -88,7 +88,7 @@ def test_batch_launch_at_defaults_above_70_percent():
     assert first[5] >= 0.70 and first[7] >= 0.70
 
 
-# ---- round 3: the same contract on this round's lines, plus what round 3 added --------------------------
+# ---- the r03_* lines: the same contract, plus the sweeps on both schedules, the clocks and the data path ----
 
 def test_r03_bench_line_contract():
     line = _line("r03_bench.json")

@@ -1,4 +1,4 @@
-"""bench.py's RCCL-native cross-check (SURVEY §8e), rehearsed at world 1.
+"""bench.py's RCCL-native cross-check, rehearsed at world 1.
 
 The cross-check compares pg_reduce_scatter with RCCL's own reduce-scatter.  It
 only means something at N > 1 (the driver's multi-GPU bench), and RCCL

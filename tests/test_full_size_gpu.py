@@ -96,7 +96,7 @@ def test_baseline_config5_sequence(gpu, lib, oracle, monkeypatch, algo):
             if dt == pgamd.DT_INT32:
                 xs = [torch.randint(-2**31, 2**31 - 1, (count,), dtype=torch.int32, device="cuda", generator=g)
                       for _ in range(world)]
-            else:   # 1 + U[-2^-10, 2^-10): stays normal over 8 factors (SURVEY.md §8d)
+            else:   # 1 + U[-2^-10, 2^-10): stays normal over 8 factors
                 xs = [1 + (torch.rand(count, dtype=torch.float64, device="cuda", generator=g) * 2 - 1) * 2.0**-10
                       for _ in range(world)]
             outs = [torch.empty(max(pgamd.block_range(count, world, r)[1], 1), dtype=xs[0].dtype, device="cuda")

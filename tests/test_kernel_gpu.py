@@ -5,7 +5,7 @@ Golden vectors come from the reference's compiled reduce_inplace
 oracle (a restatement pinned to the same vectors).  int32 and double:
 bit-exact, NaN results included (measured: gfx950 produces the same default
 NaN 0xfff8000000000000 for inf-inf / 0*inf as x86 SSE and propagates NaN
-payloads the same way; DESIGN.md §2)."""
+payloads the same way)."""
 import hashlib
 import itertools
 

@@ -37,7 +37,7 @@ def test_survey_known_answers(oracle):
     assert oracle.reduce(i(2**31 - 1), i(2**31 - 1), 0, 0)[0] == -2
     assert oracle.reduce(i(65536), i(65536), 0, 1)[0] == 0
     assert oracle.reduce(i(-123456789), i(987654), 0, 1)[0] == 1530050434
-    # W=2, R=0, chunk 4 i32, n=8 (SURVEY.md §8c)
+    # W=2, R=0, chunk 4 i32, n=8
     send = np.arange(1, 9, dtype=np.int32)
     recv = (1000 * np.arange(1, 9)).astype(np.int32)
     rc, out = oracle.mock_reduce_scatter(0, 2, 16, send, recv, 0, 0)

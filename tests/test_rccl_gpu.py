@@ -291,7 +291,7 @@ def test_collectives_match_rccl_native(gpu, world):
     """An independent pin for the W > 1 output contract: RCCL's own
     reduce-scatter / all-gather / all-reduce on the same int32 inputs give the
     same bits (sum and product), and the double sum stays within the survey's
-    tolerance of RCCL's while matching the oracle exactly."""
+    tolerance of RCCL's ((W-1) * 2^-53 * sum|x| per fold order) while matching the oracle exactly."""
     store_port = _free_port()
     results, procs = _run(world, _native_worker, lambda r: (store_port,))
     for rank, fails in results:

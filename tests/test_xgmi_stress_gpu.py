@@ -3,7 +3,7 @@ lifetime per rank: reduce-scatter / all-gather / all-reduce, int32 / double,
 sum / prod, sizes from 0 to 8 MiB, device / host / mixed buffers, in place,
 inputs that stay allocated across calls, fresh ones, and fresh allocations
 after torch.cuda.empty_cache() (which land at recycled addresses: the reuse
-hazard of DESIGN.md §5a).  Every rank draws the same sequence from one seed
+hazard: a new allocation at a freed one's address exports the same IPC handle bytes).  Every rank draws the same sequence from one seed
 and checks every call bit for bit against the oracle's ring simulator.
 
 This is the shape of the config-5 sequence (tools/xgmi_cfg5_probe.py) that
@@ -46,9 +46,10 @@ def _sequence(seed, world):
     return seq
 
 
-def _worker(rank, world, port, q, mode, seed, rings, transport="xgmi"):
+def _worker(rank, world, port, q, mode, seed, rings, transport="xgmi", tune=None):
     os.environ.update(PG_TRANSPORT=transport, PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
                       PG_CONNECT_TIMEOUT_MS="120000", PG_BARRIER_TIMEOUT_MS="60000", PG_RINGS=str(rings))
+    os.environ.update(tune or {})
     if transport == "xgmi":
         os.environ["PG_XGMI_MODE"] = mode
     else:        # the RCCL transport on one GPU: one host id per rank, hops over RCCL's socket transport
@@ -155,17 +156,24 @@ def test_xgmi_random_sequence(gpu, world, mode, seed, rings):
     assert all(p.exitcode == 0 for p in procs)
 
 
-@pytest.mark.parametrize("world,algo,seed,rings", [(3, "direct", 11, 2), (4, "ring", 12, 2), (2, "direct", 13, 1),
-                                                   (4, "direct", 14, 4)])
-def test_rccl_random_sequence(gpu, world, algo, seed, rings):
+SMALL_GROUPS = {"PG_CHUNK_BYTES": "65536", "PG_INFLIGHT": "2"}     # many transport groups per round
+
+
+@pytest.mark.parametrize("world,algo,seed,rings,tune", [
+    (3, "direct", 11, 2, None), (4, "ring", 12, 2, None), (2, "direct", 13, 1, None), (4, "direct", 14, 4, None),
+    (4, "ring", 15, 2, dict(SMALL_GROUPS, PG_REDUCE_BYTES="393216")), (3, "ring", 16, 4, dict(SMALL_GROUPS, PG_REDUCE_BYTES="0")),
+    (4, "direct", 17, 2, dict(SMALL_GROUPS, PG_REDUCE_BYTES="262144"))])
+def test_rccl_random_sequence(gpu, world, algo, seed, rings, tune):
     """The same random sequence over the RCCL transport (ring and direct
     schedules; eager sizes, host / device / mixed buffers, in place, recycled
-    allocations), every call against the oracle ring."""
+    allocations), every call against the oracle ring.  tune: small segments, so
+    that a round is many transport groups, with the reduce launch taken per
+    group (PG_REDUCE_BYTES=0) or once a few groups are pending."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, algo, seed, rings, "rccl")) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, algo, seed, rings, "rccl", tune)) for r in range(world)]
     for p in procs:
         p.start()
     results = []

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(B) void k_dyn(f64x2* __restrict__ d, const f64x2* _
 }
 
 
-// Per-XCD queues (round 2, second attempt): the one-shot grid keeps one tile
+// Per-XCD queues (second attempt): the one-shot grid keeps one tile
 // per block, but blocks from `prefix` on take their tile from the queue of
 // the XCD they run on (HW_REG_XCC_ID), and from the other XCDs' queues once
 // their own is empty.  The grid has `slack` more blocks than tiles, so a

@@ -1,7 +1,7 @@
 // tools/lab/reduce_lab.hip -- EXPERIMENTS ONLY (not part of libpg_amd.so).
 //
 // Variants of the double-sum streaming reduce used to decide the shipped
-// kernel's cache policy and geometry (DESIGN.md "Kernel tuning").  Buffer
+// kernel's cache policy and geometry.  Buffer
 // loads/stores with explicit gfx950 cache-policy bits (aux: 1 = sc0,
 // 2 = nt, 16 = sc1), block sizes, an XCD-contiguous block remap and the load
 // order.  One tile per block (one-shot grid); n must be a multiple of the tile.
