@@ -232,6 +232,48 @@ def kernel_leg(lib, args, rank, world):
     return t1 - t0, region_mean_ms, stamped
 
 
+def sustained_leg(lib, rank, world, seconds=2.0, batch=200):
+    """The config-2 launch held for `seconds` on every GPU at once (the timed
+    steps above last a few milliseconds): back-to-back pgk_reduce launches of
+    256 MiB doubles over 4 rotating pairs, one HIP event per `batch` launches.
+    Reports the rate of every batch window (min / median / max over windows,
+    slowest rank per window) so that a clock or thermal droop over time shows."""
+    pool = torch.empty(2 * N_PAIRS * N_ELEMS, dtype=torch.float64, device="cuda")
+    pool.uniform_(-1e-3, 1e-3, generator=torch.Generator(device="cuda").manual_seed(4321 + rank))
+    base, size = pool.data_ptr(), N_ELEMS * 8
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    nbatches = max(2, int(seconds / (batch * 125e-6)))
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nbatches + 1)]
+    for i in range(8):
+        lib.pgk_reduce(base + 2 * size * (i % N_PAIRS), base + 2 * size * (i % N_PAIRS) + size, N_ELEMS, DT, OP, sh)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    k = 0
+    for b in range(nbatches):
+        for _ in range(batch):
+            d = base + 2 * size * (k % N_PAIRS)
+            k += 1
+            if lib.pgk_reduce(d, d + size, N_ELEMS, DT, OP, sh) != 0:
+                raise RuntimeError(pgamd.last_error())
+        evs[b + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    per = [evs[b].elapsed_time(evs[b + 1]) / batch for b in range(nbatches)]          # ms per launch, per window
+    worst = [max_over_ranks(v, world) for v in per]                                    # slowest rank per window
+    gbs = [3 * size / (v * 1e-3) / 1e9 for v in worst]
+    del pool
+    torch.cuda.empty_cache()
+    return {"seconds": round(max_over_ranks(wall, world), 2), "launches": nbatches * batch, "window_launches": batch,
+            "frac_min": round(min(gbs) / HBM_PEAK_GBS, 4), "frac_median": round(float(np.median(gbs)) / HBM_PEAK_GBS, 4),
+            "frac_max": round(max(gbs) / HBM_PEAK_GBS, 4), "frac_first_window": round(gbs[0] / HBM_PEAK_GBS, 4),
+            "frac_last_window": round(gbs[-1] / HBM_PEAK_GBS, 4),
+            "note": "256 MiB double sum, back-to-back launches (kernel boundaries included), every rank at once; "
+                    "each window = window_launches launches between two HIP events, slowest rank per window"}
+
+
 # per operand: the in-ring launch sizes (4-32 MiB: PG_CHUNK_BYTES x PG_INFLIGHT) and north_star's >= 64 MiB
 SWEEP_BYTES = (4 << 20, 16 << 20, 32 << 20, 64 << 20, 128 << 20, 256 << 20, 512 << 20, 1 << 30)
 SWEEP_POOL = 4 << 30
@@ -1101,6 +1143,15 @@ def main():
     achieved_gbs = bytes_per_step / (mean_launch_ms * 1e-3) / 1e9
     value = world * bytes_per_step * args.steps / wall_max / GIB
 
+    sustained = None
+    if not args.no_sizes:
+        progress(rank, "sustained kernel leg")
+        with leg_clock("kernel_sustained"):
+            try:
+                sustained = sustained_leg(lib, rank, world)
+            except Exception as e:  # noqa: BLE001 -- reported, never fatal for the primary line
+                sustained = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     host = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -1149,6 +1200,7 @@ def main():
                              "median": round(bytes_per_step / float(np.median(per_rank_ms)) / 1e6, 1),
                              "max": round(bytes_per_step / min(per_rank_ms) / 1e6, 1)}},
             "kernel_sizes": sizes,
+            "kernel_sustained": sustained,
             "cpu_baseline": cpu,
             "host_staged": host,
             "config1": cfg1,
