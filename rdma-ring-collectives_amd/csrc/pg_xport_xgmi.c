@@ -1038,6 +1038,7 @@ int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
    * the end: all ranks fail together instead of the healthy ones waiting out
    * the barrier timeout for the one that left. */
   int rc = 0, lost = 0;
+  const char *fail_hook = getenv("PG_XGMI_FAIL_PROBE");     /* test hook: this rank's phase 1 fails */
   for (int phase = 0; phase < 4; ++phase) {
     void *dst[16];
     const void *src[16];
@@ -1054,6 +1055,10 @@ int pgx_xgmi_link_probe(void *pg_handle, size_t bytes, int reps, double *gbs) {
       nb[k++] = part;
     }
     if (barrier(pg)) { lost = 1; break; }
+    if (rc == 0 && phase == 1 && fail_hook && *fail_hook && atoi(fail_hook) == r) {
+      pg_set_error("xgmi probe: failure injected on rank %d (PG_XGMI_FAIL_PROBE)", r);
+      rc = -1;
+    }
     if (rc == 0 && pgk_gather(dst, src, nb, k, (void *)im->red)) { pg_set_error("xgmi probe: %s", pgk_last_error()); rc = -1; }
     if (rc == 0 && (hipEventRecord(e0, im->red) != hipSuccess)) rc = -1;
     for (int i = 0; rc == 0 && i < reps; ++i)

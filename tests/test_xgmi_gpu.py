@@ -316,9 +316,9 @@ def test_xgmi_ipc_bit31_sizes(gpu):
         assert not fails, (rank, fails)
 
 
-def _release_worker(rank, world, port, q):
+def _release_worker(rank, world, port, q, push=False):
     os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
-                      PG_BARRIER_TIMEOUT_MS="60000")
+                      PG_BARRIER_TIMEOUT_MS="60000", PG_XGMI_MODE="push" if push else "read")
     sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
     res = {}
     try:
@@ -341,21 +341,42 @@ def _release_worker(rank, world, port, q):
         torch.cuda.synchronize()
         res["free0"] = torch.cuda.mem_get_info()[0]
         sync_all()
-        count = 1 << 29                                   # 4 GiB of doubles, read in place by the peers
-        x = torch.full((count,), float(rank + 1), dtype=torch.float64, device="cuda")
-        off, ln = pgamd.block_range(count, world, rank)
-        out = torch.empty(ln, dtype=torch.float64, device="cuda")
-        assert lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, 1, 0, h) == 0, pgamd.last_error()
-        res["zero_copy"] = pgamd.stats(h)["zero_copy"]
-        res["ok"] = bool((out == world * (world + 1) / 2).all())
+        if not push:
+            count = 1 << 29                               # 4 GiB of doubles, read in place by the peers
+            x = torch.full((count,), float(rank + 1), dtype=torch.float64, device="cuda")
+            off, ln = pgamd.block_range(count, world, rank)
+            out = torch.empty(ln, dtype=torch.float64, device="cuda")
+            assert lib.pg_reduce_scatter(x.data_ptr(), out.data_ptr(), count, 1, 0, h) == 0, pgamd.last_error()
+            res["zero_copy"] = pgamd.stats(h)["zero_copy"]
+            res["ok"] = bool((out == world * (world + 1) / 2).all())
+        else:
+            # push mode: an all-gather still READS its peers' inputs (and caches the
+            # mappings of a 1 GiB allocation here; 2 GiB ones are never exported, their
+            # size has bit 31 set); the calls after it are pushed
+            count = 1 << 27
+            x = torch.full((count,), float(rank + 1), dtype=torch.float64, device="cuda")
+            out = torch.empty(count * world, dtype=torch.float64, device="cuda")
+            assert lib.pg_all_gather(x.data_ptr(), out.data_ptr(), count, 1, h) == 0, pgamd.last_error()
+            res["zero_copy"] = pgamd.stats(h)["zero_copy"]
+            res["ok"] = all(bool((out[q * count:(q + 1) * count] == q + 1).all()) for q in range(world))
         del x, out
         torch.cuda.empty_cache()                          # the caller frees its large input
-        for kind in ("in place", "slot copy"):            # the next calls read other inputs
-            y = torch.full((1 << 20,), 2.0, dtype=torch.float64, device="cuda")
-            z = y if kind == "slot copy" else torch.empty(1 << 20, dtype=torch.float64, device="cuda")
-            assert lib.pg_all_reduce(y.data_ptr(), z.data_ptr(), 1 << 20, 1, 0, h) == 0, pgamd.last_error()
-            res["ok"] &= bool((z == 2.0 * world).all())
-            del y, z
+        if not push:
+            for kind in ("in place", "slot copy"):        # the next calls read other inputs
+                y = torch.full((1 << 20,), 2.0, dtype=torch.float64, device="cuda")
+                z = y if kind == "slot copy" else torch.empty(1 << 20, dtype=torch.float64, device="cuda")
+                assert lib.pg_all_reduce(y.data_ptr(), z.data_ptr(), 1 << 20, 1, 0, h) == 0, pgamd.last_error()
+                res["ok"] &= bool((z == 2.0 * world).all())
+                del y, z
+        else:
+            for _ in range(2):                            # pushed calls: no peer input is read at all
+                n = 1 << 21
+                y = torch.full((n,), 2.0, dtype=torch.float64, device="cuda")
+                o2, l2 = pgamd.block_range(n, world, rank)
+                z = torch.empty(l2, dtype=torch.float64, device="cuda")
+                assert lib.pg_reduce_scatter(y.data_ptr(), z.data_ptr(), n, 1, 0, h) == 0, pgamd.last_error()
+                res["ok"] &= bool((z == 2.0 * world).all()) and pgamd.stats(h)["zero_copy"] == 0
+                del y, z
         sync_all()
         torch.cuda.synchronize()
         res["free1"] = torch.cuda.mem_get_info()[0]
@@ -366,18 +387,22 @@ def _release_worker(rank, world, port, q):
     q.put((rank, res))
 
 
-def test_xgmi_freed_large_input_is_released(gpu):
-    """A peer's mapping of a caller's 4 GiB input must not keep that HBM alive
-    once the caller has freed it and moved on: the next call (read in place or
-    slot copy) closes large mappings it does not read.  Both ranks share the
-    one GPU, so device free memory after the sequence must be back to where it
-    was before the 4 GiB inputs (within 1 GiB of small allocations)."""
+@pytest.mark.parametrize("push", [False, True])
+def test_xgmi_freed_large_input_is_released(gpu, push):
+    """A peer's mapping of a caller's large input (4 GiB; 1 GiB per rank in the
+    push case) must not keep that HBM alive once the caller has freed it and moved
+    on: the next call closes large mappings it does not read, whether it reads
+    other inputs in place, takes the slot copy, or (push mode, where an
+    all-gather cached the mapping) pushes and reads no peer input at all.  Both
+    ranks share the one GPU, so device free memory after the sequence must be
+    back to where it was before the large inputs (within 1 GiB of small
+    allocations)."""
     import torch.multiprocessing as mp
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_release_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_release_worker, args=(r, world, port, q, push)) for r in range(world)]
     for p in procs:
         p.start()
     results = []
@@ -655,3 +680,58 @@ def test_xgmi_failed_import_is_redone_with_copy(gpu):
     assert "hipIpcOpenMemHandle" in errs[0], errs       # the injected failure happened, and was absorbed
     for rank, out in results:                           # by every rank redoing the first call, only that one
         assert out["retried"] == [1, 0, 0, 0], (rank, out["retried"])
+
+
+def _probe_fail_worker(rank, world, port, q):
+    os.environ.update(PG_TRANSPORT="xgmi", PG_RANK=str(rank), PG_DEVICE="0", PG_PORT=str(port),
+                      PG_BARRIER_TIMEOUT_MS="120000", PG_XGMI_MODE="auto", PG_XGMI_FAIL_PROBE="1")
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    out = {}
+    try:
+        import ctypes
+        import time
+
+        import torch
+
+        import pgamd
+        torch.cuda.set_device(0)
+        lib = pgamd.load()
+        h = ctypes.c_void_p()
+        t0 = time.monotonic()
+        out["rc"] = lib.connect_process_group(" ".join(["127.0.0.1"] * world).encode(), ctypes.byref(h))
+        out["took"] = time.monotonic() - t0
+        out["err"] = pgamd.last_error()
+        if out["rc"] == 0:
+            lib.pg_close(h)
+    except Exception as e:  # noqa: BLE001
+        out["exception"] = repr(e)
+    q.put((rank, out))
+
+
+def test_xgmi_probe_failure_fails_connect_on_every_rank_together(gpu):
+    """The connect-time link probe of the auto mode: when one rank's probe launch
+    fails (test hook PG_XGMI_FAIL_PROBE), that rank keeps meeting the others at
+    the probe's barriers and the outcome is agreed at its end, so every rank's
+    connect_process_group returns -1 within seconds -- nobody sits in a barrier
+    until PG_BARRIER_TIMEOUT_MS (120 s here)."""
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_probe_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in range(world):
+            results.append(q.get(timeout=200))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, out in results:
+        assert out.get("rc") == -1, (rank, out)
+        assert out["took"] < 60.0, (rank, out)
+        assert "probe" in out["err"], (rank, out)
