@@ -127,6 +127,25 @@ PG_API int pg_plan_all_gather(int rank, int world, int count, int datatype, int 
 PG_API int pg_plan_direct_reduce_scatter(int rank, int world, int count, int datatype, size_t chunk_bytes,
                                          int inflight, int rings, struct pg_step *steps, int max_steps);
 
+/* The reduce launches of a set of ring steps.  The executor does not reduce a
+ * transport group's arrived segments at once: steps wait until PG_REDUCE_BYTES
+ * per operand are pending (or the round ends) and are then reduced together.
+ * This lists what that one launch covers: idx[0..n) are indices into st[] of
+ * steps with red_elems > 0; they are sorted in place by (buffers, direction,
+ * destination offset), and every run of steps contiguous in both operands
+ * becomes one range (the segments of one ring over consecutive groups are
+ * neighbours in the same block, so usually one range per ring).  elem_size: 4
+ * or 8.  Returns the number of ranges written to out[0..max_out), or -1 when
+ * max_out is too small or an argument is bad. */
+struct pg_red_range {
+  int32_t dst_buf, src_buf;   /* PG_BUF_*                                        */
+  int32_t rev, pad;           /* rev: dst = src op dst (pg_step.red_rev)         */
+  int64_t dst_off, src_off;   /* bytes                                           */
+  int64_t elems;
+};
+PG_API int pg_plan_coalesce(const struct pg_step *st, int *idx, int n, size_t elem_size,
+                            struct pg_red_range *out, int max_out);
+
 /* Open a handle without a server list: transport LOOPBACK (reference mock
  * semantics for a given rank/world) or SELF (world must be 1).  The device is
  * the current HIP device. */

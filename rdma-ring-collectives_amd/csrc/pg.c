@@ -320,6 +320,7 @@ void pg_impl_destroy(struct pg *pg) {
   if (im->comm) hipStreamDestroy(im->comm);
   if (im->red) hipStreamDestroy(im->red);
   free(im->pend);
+  free(im->ranges);
   for (int i = 0; i < 2; ++i) if (im->stage[i]) hipFree(im->stage[i]);
   if (im->dsrc) hipFree(im->dsrc);
   if (im->dout) hipFree(im->dout);

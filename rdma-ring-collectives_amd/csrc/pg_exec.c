@@ -129,24 +129,11 @@ static int red_flush(struct pg_impl *im, struct red_batch *rb, int dt, int op, h
   return 0;
 }
 
-/* Pending reduce steps ordered so that neighbours in memory are neighbours in
- * the list: by operand buffers and direction, then by destination offset. */
-/* qsort has no context argument: the plan being sorted, per calling thread */
-static __thread const struct pg_step *t_sort_steps;
-static int pend_cmp(const void *pa, const void *pb) {
-  const struct pg_step *a = &t_sort_steps[*(const int *)pa], *b = &t_sort_steps[*(const int *)pb];
-  if (a->red_dst_buf != b->red_dst_buf) return a->red_dst_buf < b->red_dst_buf ? -1 : 1;
-  if (a->red_src_buf != b->red_src_buf) return a->red_src_buf < b->red_src_buf ? -1 : 1;
-  if (a->red_rev != b->red_rev) return a->red_rev < b->red_rev ? -1 : 1;
-  if (a->red_dst_off != b->red_dst_off) return a->red_dst_off < b->red_dst_off ? -1 : 1;
-  return 0;
-}
-
 /* Reduce every pending step: the comm stream's position (behind the last
- * group that carried any of them) gates the reduce stream, runs of
- * steps contiguous in both operands become one range each -- the segments of
- * one ring over consecutive batches are neighbours in the same block -- and
- * all ranges go out in one pgk_reduce_ranges launch (eight ranges at most per
+ * group that carried any of them) gates the reduce stream, pg_plan_coalesce
+ * turns the steps into ranges contiguous in both operands -- the segments of
+ * one ring over consecutive groups are neighbours in the same block -- and all
+ * ranges go out in one pgk_reduce_ranges launch (eight ranges at most per
  * launch).  Then every step's red_ev is recorded behind it. */
 static int reduce_pending(struct pg_impl *im, const struct pg_step *st, int npend, int nb, void *const bufs[5],
                           int dt, int op) {
@@ -155,38 +142,31 @@ static int reduce_pending(struct pg_impl *im, const struct pg_step *st, int npen
   hipEvent_t rev = im->recv_ev[nb % PG_RECV_EVENTS];
   PG_CHECK_HIP(hipEventRecord(rev, im->comm));
   PG_CHECK_HIP(hipStreamWaitEvent(rs, rev, 0));
-  t_sort_steps = st;
-  qsort(im->pend, (size_t)npend, sizeof(int), pend_cmp);
+  if (npend > im->ranges_cap) {
+    struct pg_red_range *rr = (struct pg_red_range *)realloc(im->ranges, sizeof(*rr) * (size_t)npend);
+    if (!rr) { pg_set_error("pg_exec: out of host memory"); return -1; }
+    im->ranges = rr;
+    im->ranges_cap = npend;
+  }
+  const int nr = pg_plan_coalesce(st, im->pend, npend, pg_elem_size(dt), im->ranges, im->ranges_cap);
+  if (nr < 0) { pg_set_error("pg_exec: could not list the pending reduces"); return -1; }
   struct red_batch rb;
   rb.k = 0;
-  const int64_t es = pg_elem_size(dt);
-  int u = 0;
-  while (u < npend) {
-    const struct pg_step *s0 = &st[im->pend[u]];
-    int64_t elems = s0->red_elems;
-    int v = u + 1;
-    while (v < npend) {
-      const struct pg_step *s1 = &st[im->pend[v]];
-      if (s1->red_rev != s0->red_rev || s1->red_dst_buf != s0->red_dst_buf || s1->red_src_buf != s0->red_src_buf ||
-          s1->red_dst_off != s0->red_dst_off + elems * es || s1->red_src_off != s0->red_src_off + elems * es)
-        break;
-      elems += s1->red_elems;
-      ++v;
-    }
-    char *dst = at(bufs, s0->red_dst_buf, s0->red_dst_off);
-    const char *src = at(bufs, s0->red_src_buf, s0->red_src_off);
-    /* the arrival is the left operand: dst = dst op src, or with red_rev
-     * (the arrival sits in src) dst = src op dst */
+  for (int u = 0; u < nr; ++u) {
+    const struct pg_red_range *g = &im->ranges[u];
+    char *dst = at(bufs, g->dst_buf, g->dst_off);
+    const char *src = at(bufs, g->src_buf, g->src_off);
+    /* the arrival is the left operand: dst = dst op src, or with rev (the
+     * arrival sits in src) dst = src op dst */
     rb.out[rb.k] = dst;
-    rb.a[rb.k] = s0->red_rev ? src : dst;
-    rb.b[rb.k] = s0->red_rev ? dst : src;
-    rb.n[rb.k] = (size_t)elems;
-    im->stats.reduce_elems += elems;
+    rb.a[rb.k] = g->rev ? src : dst;
+    rb.b[rb.k] = g->rev ? dst : src;
+    rb.n[rb.k] = (size_t)g->elems;
+    im->stats.reduce_elems += g->elems;
     if (++rb.k == PG_RED_RANGES && red_flush(im, &rb, dt, op, rs)) return -1;
-    u = v;
   }
   if (red_flush(im, &rb, dt, op, rs)) return -1;
-  for (u = 0; u < npend; ++u) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[im->pend[u]].seg], rs));
+  for (int u = 0; u < npend; ++u) PG_CHECK_HIP(hipEventRecord(im->red_ev[st[im->pend[u]].seg], rs));
   return 0;
 }
 

@@ -66,6 +66,7 @@ struct pg_impl {
   size_t red_bytes;           /* PG_REDUCE_BYTES: arrived segments are reduced once this many
                                  bytes per operand are pending (or the round ends); 0 = per batch */
   int *pend; int pend_cap;    /* plan steps whose reduce is pending            */
+  struct pg_red_range *ranges; int ranges_cap;   /* what the next reduce launch covers */
   hipEvent_t *red_ev;         /* per segment: its reduce finished             */
   int n_red_ev;
   hipEvent_t recv_ev[PG_RECV_EVENTS]; /* per batch: its receives landed       */

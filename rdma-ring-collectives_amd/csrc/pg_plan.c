@@ -26,6 +26,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "pg.h"
@@ -361,4 +362,50 @@ int pg_plan_all_gather(int rank, int world, int count, int datatype, int uniform
   }
   if (steps && n > max_steps) return -1;
   return n;
+}
+
+/* ---- which steps reduce together ---------------------------------------------- */
+
+/* qsort has no context argument: the plan being sorted, per calling thread */
+static __thread const struct pg_step *t_sort_steps;
+
+static int red_order(const void *pa, const void *pb) {
+  const struct pg_step *a = &t_sort_steps[*(const int *)pa], *b = &t_sort_steps[*(const int *)pb];
+  if (a->red_dst_buf != b->red_dst_buf) return a->red_dst_buf < b->red_dst_buf ? -1 : 1;
+  if (a->red_src_buf != b->red_src_buf) return a->red_src_buf < b->red_src_buf ? -1 : 1;
+  if (a->red_rev != b->red_rev) return a->red_rev < b->red_rev ? -1 : 1;
+  if (a->red_dst_off != b->red_dst_off) return a->red_dst_off < b->red_dst_off ? -1 : 1;
+  return 0;
+}
+
+int pg_plan_coalesce(const struct pg_step *st, int *idx, int n, size_t elem_size,
+                     struct pg_red_range *out, int max_out) {
+  if (n < 0 || (n && (!st || !idx || !out)) || (elem_size != 4 && elem_size != 8)) return -1;
+  t_sort_steps = st;
+  qsort(idx, (size_t)n, sizeof(int), red_order);
+  const int64_t es = (int64_t)elem_size;
+  int k = 0, u = 0;
+  while (u < n) {
+    const struct pg_step *s0 = &st[idx[u]];
+    int64_t elems = s0->red_elems;
+    int v = u + 1;
+    for (; v < n; ++v) {
+      const struct pg_step *s1 = &st[idx[v]];
+      if (s1->red_rev != s0->red_rev || s1->red_dst_buf != s0->red_dst_buf || s1->red_src_buf != s0->red_src_buf ||
+          s1->red_dst_off != s0->red_dst_off + elems * es || s1->red_src_off != s0->red_src_off + elems * es)
+        break;
+      elems += s1->red_elems;
+    }
+    if (k == max_out) return -1;
+    out[k].dst_buf = s0->red_dst_buf;
+    out[k].src_buf = s0->red_src_buf;
+    out[k].rev = s0->red_rev;
+    out[k].pad = 0;
+    out[k].dst_off = s0->red_dst_off;
+    out[k].src_off = s0->red_src_off;
+    out[k].elems = elems;
+    ++k;
+    u = v;
+  }
+  return k;
 }

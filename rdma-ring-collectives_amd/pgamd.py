@@ -50,6 +50,13 @@ class PgStep(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class PgRedRange(ctypes.Structure):
+    """struct pg_red_range (include/pg_ext.h)."""
+    _fields_ = [("dst_buf", ctypes.c_int32), ("src_buf", ctypes.c_int32), ("rev", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("dst_off", ctypes.c_int64), ("src_off", ctypes.c_int64),
+                ("elems", ctypes.c_int64)]
+
+
 class PgStats(ctypes.Structure):
     """struct pg_stats (include/pg_ext.h)."""
     _fields_ = [
@@ -92,6 +99,7 @@ _SIGS = {
     "pg_plan_direct_reduce_scatter": (_I, [_I, _I, _I, _I, _SZ, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_plan_all_gather": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(PgStep), _I]),
     "pg_block_part": (_I, [_SZ, _I, _I, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "pg_plan_coalesce": (_I, [ctypes.POINTER(PgStep), ctypes.POINTER(_I), _I, _SZ, ctypes.POINTER(PgRedRange), _I]),
     "pg_ring_offset": (_I, [_I, _I, _I]),
     "pgx_xgmi_link_probe": (_I, [_VP, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
     "pgx_xgmi_mode": (_I, [_VP, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
@@ -210,6 +218,23 @@ def plan_all_gather(rank, world, count, dt, uniform=1, rings=2):
     arr = (PgStep * max(n, 1))()
     lib.pg_plan_all_gather(rank, world, count, dt, uniform, rings, arr, n)
     return [arr[i].as_dict() for i in range(n)]
+
+
+def plan_coalesce(steps, es):
+    """pg_plan_coalesce on a list of step dicts (as the plan_* helpers return
+    them): the ranges one reduce launch over those steps covers, as dicts."""
+    lib = load()
+    n = len(steps)
+    arr = (PgStep * max(n, 1))()
+    for i, s in enumerate(steps):
+        for name, _ in PgStep._fields_:
+            setattr(arr[i], name, s.get(name, 0))
+    idx = (ctypes.c_int * max(n, 1))(*range(n))
+    out = (PgRedRange * max(n, 1))()
+    k = lib.pg_plan_coalesce(arr, idx, n, es, out, n)
+    if k < 0:
+        raise ValueError("pg_plan_coalesce: bad arguments")
+    return [{name: getattr(out[i], name) for name, _ in PgRedRange._fields_} for i in range(k)]
 
 
 def head(handle) -> PgHead:

@@ -36,6 +36,33 @@ int main(void) {
                           (size_t)(st[i].recv_off + st[i].recv_bytes) > stage * es) return 5;
                       if (st[i].recv_buf == PG_BUF_OUT && (size_t)(st[i].recv_off + st[i].recv_bytes) > blk * es) return 6;
                     }
+                    /* the reduce launches (pg_plan_coalesce): every round's reduce steps, handed over
+                     * in reverse, must come back as ranges that cover each element once, inside the
+                     * buffers, never more ranges than steps */
+                    {
+                      int *idx = malloc(sizeof(int) * (n ? n : 1));
+                      struct pg_red_range *rr = malloc(sizeof(*rr) * (n ? n : 1));
+                      for (int k = 0; k + 1 < W; ++k) {
+                        int m2 = 0;
+                        long long want = 0, got = 0;
+                        for (int i = n - 1; i >= 0; --i)
+                          if (st[i].round == k && st[i].red_elems > 0) { idx[m2++] = i; want += st[i].red_elems; }
+                        int nr = pg_plan_coalesce(st, idx, m2, es, rr, m2 ? m2 : 1);
+                        if (nr < 0 || nr > m2) return 12;
+                        for (int u = 0; u < nr; ++u) {
+                          got += rr[u].elems;
+                          if (rr[u].elems <= 0 || rr[u].dst_off < 0 || rr[u].src_off < 0) return 13;
+                          if (rr[u].src_buf == PG_BUF_SRC && (size_t)(rr[u].src_off + rr[u].elems * (long long)es) > counts[ci] * es) return 14;
+                          if (u && rr[u].dst_buf == rr[u - 1].dst_buf && rr[u].src_buf == rr[u - 1].src_buf &&
+                              rr[u].rev == rr[u - 1].rev && rr[u].dst_off < rr[u - 1].dst_off + rr[u - 1].elems * (long long)es)
+                            return 15;                       /* sorted, not overlapping */
+                        }
+                        if (got != want) return 16;
+                      }
+                      if (pg_plan_coalesce(st, idx, 1, 3, rr, 1) != -1) return 17;    /* bad element size */
+                      free(idx);
+                      free(rr);
+                    }
                     total += n;
                     free(st);
                     if (!alias && !eager) {           /* the direct exchange (no alias / eager knobs) */

@@ -67,11 +67,29 @@ def direct_fold(bufs, s, rank, world, dt, op):
     _view(bufs, s["red_dst_buf"], s["red_dst_off"], n).view(NP[dt])[:] = acc
 
 
-def run_plans(plans, bufs_per_rank, dt, op):
+def _reduce_ranges(bufs, steps, es, dt, op):
+    """One reduce launch of the executor over `steps`: the library's own
+    pg_plan_coalesce lists the ranges, numpy reduces each."""
+    total = 0
+    for g in pgamd.plan_coalesce(steps, es):
+        d = _view(bufs, g["dst_buf"], g["dst_off"], g["elems"] * es).view(NP[dt])
+        src = _view(bufs, g["src_buf"], g["src_off"], g["elems"] * es).view(NP[dt])
+        np_reduce(d, src, op, g["rev"])
+        total += g["elems"]
+    assert total == sum(s["red_elems"] for s in steps)          # nothing lost, nothing twice
+    return len(steps)
+
+
+def run_plans(plans, bufs_per_rank, dt, op, red_bytes=None):
     """Execute every rank's step list.  bufs_per_rank[r][PG_BUF_*] = uint8 arrays.
     A step runs once all its receives are available; sends snapshot the bytes
     at send time (a rank's steps run in order, so a forwarded partial is
-    already reduced, as the executor's red_ev wait guarantees)."""
+    already reduced, as the executor's red_ev wait guarantees).
+    red_bytes = None: every step reduces on arrival.  Otherwise the executor's
+    rule (csrc/pg_exec.c, PG_REDUCE_BYTES): a batch's reduce steps wait until
+    red_bytes per operand are pending, or the round or the plan ends, and are
+    then reduced range by range as pg_plan_coalesce lists them.  Returns the
+    number of reduce launches per rank (ring steps only)."""
     world = len(plans)
     chans = {(a, b): deque() for a in range(world) for b in range(world)}     # directed edge a -> b
     pos = [0] * world
@@ -87,6 +105,8 @@ def run_plans(plans, bufs_per_rank, dt, op):
         batches.append(bl)
     es = 4 if dt == 0 else 8
     pending = [None] * world      # sends of a batch are posted before its receives
+    waiting = [[] for _ in range(world)]          # reduce steps not launched yet (red_bytes mode)
+    launches = [0] * world
     progress = True
     while progress:
         progress = False
@@ -97,6 +117,10 @@ def run_plans(plans, bufs_per_rank, dt, op):
             bufs = bufs_per_rank[r]
             if pending[r] is None:
                 for s in batch:
+                    # a forwarded partial was reduced in the previous round: no step of an
+                    # earlier round may still wait for its launch when this round sends
+                    assert not (s["send_bytes"] and s.get("send_wait") and
+                                any(w["round"] < s["round"] for w in waiting[r])), (r, s)
                     if s["send_bytes"]:
                         chans[(r, (r + s["send_peer"]) % world)].append(
                             _view(bufs, s["send_buf"], s["send_off"], s["send_bytes"]).copy())
@@ -117,18 +141,31 @@ def run_plans(plans, bufs_per_rank, dt, op):
             for s in batch:
                 if s.get("red_fold"):
                     direct_fold(bufs, s, r, world, dt, op)
-                elif s["red_elems"]:
+                elif s["red_elems"] and red_bytes is None:
                     d = _view(bufs, s["red_dst_buf"], s["red_dst_off"], s["red_elems"] * es).view(NP[dt])
                     src = _view(bufs, s["red_src_buf"], s["red_src_off"], s["red_elems"] * es).view(NP[dt])
                     np_reduce(d, src, op, s.get("red_rev", 0))
+                    launches[r] += 1
+                elif s["red_elems"]:
+                    waiting[r].append(s)
+            if waiting[r]:
+                last = pos[r] + 1 == len(batches[r])
+                round_ends = last or batches[r][pos[r] + 1][0]["round"] != batch[0]["round"]
+                if round_ends or sum(s["red_elems"] for s in waiting[r]) * es >= red_bytes:
+                    _reduce_ranges(bufs, waiting[r], es, dt, op)
+                    launches[r] += 1
+                    waiting[r] = []
             pos[r] += 1
             pending[r] = None
             progress = True
     assert all(pos[r] == len(batches[r]) for r in range(world)), "deadlock"
     assert all(len(c) == 0 for c in chans.values()), "unconsumed messages"
+    assert not any(waiting), "reduce steps left pending"
+    return launches
 
 
-def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False, rings=2):
+def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, alias=False, rings=2, red_bytes=None,
+                        launches_out=None):
     world, count = len(sends), sends[0].size
     es = 4 if dt == 0 else 8
     blk = -(-count // world) if count else 0
@@ -145,7 +182,9 @@ def ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, 
             out = np.zeros(ln * es, np.uint8)
         bufs.append({pgamd.PG_BUF_SRC: src, pgamd.PG_BUF_OUT: out,
                      pgamd.PG_BUF_STAGE0: np.zeros(bmax, np.uint8), pgamd.PG_BUF_STAGE1: np.zeros(bmax, np.uint8)})
-    run_plans(plans, bufs, dt, op)
+    launches = run_plans(plans, bufs, dt, op, red_bytes)
+    if launches_out is not None:
+        launches_out[:] = launches
     return [bufs[r][pgamd.PG_BUF_OUT].view(NP[dt]).copy() for r in range(world)], bufs
 
 
@@ -162,9 +201,10 @@ def ring_all_gather(sends, dt, rings=2):
     return [b[pgamd.PG_BUF_OUT].view(NP[dt]).copy() for b in bufs]
 
 
-def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, rings=2):
+def ring_all_reduce(sends, dt, op, chunk_bytes, eager_max=4096, inflight=4, rings=2, red_bytes=None):
     world, count = len(sends), sends[0].size
-    _, bufs = ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max, inflight, alias=True, rings=rings)
+    _, bufs = ring_reduce_scatter(sends, dt, op, chunk_bytes, eager_max, inflight, alias=True, rings=rings,
+                                  red_bytes=red_bytes)
     plans = [pgamd.plan_all_gather(r, world, count, dt, 0, rings) for r in range(world)]
     agbufs = [{pgamd.PG_BUF_OUT: bufs[r][pgamd.PG_BUF_SRC]} for r in range(world)]
     run_plans(plans, agbufs, dt, 0)

@@ -228,3 +228,55 @@ def test_plans_refuse_absurd_step_counts(lib):
     assert lib.pg_plan_direct_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4, 1, 2, None, 0) == -1
     assert lib.pg_plan_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4 << 20, 0, 4, 2, 0, None, 0) > 0
     assert lib.pg_plan_direct_reduce_scatter(0, 8, (1 << 30) + 1, 0, 4 << 20, 4, 2, None, 0) > 0
+
+
+@pytest.mark.parametrize("rings", [1, 2, 4])
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
+def test_deferred_reduce_launches_match_oracle(oracle, world, rings):
+    """The executor's rule for its reduce launches (csrc/pg_exec.c,
+    PG_REDUCE_BYTES), run in numpy over the library's own plans and its own
+    pg_plan_coalesce: a transport group's reduce steps wait until red_bytes per
+    operand are pending, or the round ends, and are reduced range by range.
+    Whatever the threshold -- every group on its own, a few groups, the whole
+    round -- the bits are the oracle ring's, in place too, and a larger
+    threshold never means more launches."""
+    for dt, op, count in itertools.product((0, 1), (0, 1), (7, 1001, 4099)):
+        xs = inputs(oracle, world, count, dt, op, 500 + count)
+        want_rs = oracle.ring_reduce_scatter(xs, dt, op, rings)
+        want_ar = oracle.ring_all_reduce(xs, dt, op, rings)
+        counts = []
+        for red_bytes in (0, 96, 1000, 1 << 30):
+            n = [0] * world
+            got, _ = ring_reduce_scatter(xs, dt, op, 24, eager_max=0, inflight=2, rings=rings, red_bytes=red_bytes,
+                                         launches_out=n)
+            for r in range(world):
+                assert got[r].tobytes() == want_rs[r].tobytes(), (world, rings, r, dt, op, count, red_bytes)
+            counts.append(sum(n))
+            got = ring_all_reduce(xs, dt, op, 24, eager_max=0, inflight=2, rings=rings, red_bytes=red_bytes)
+            for r in range(world):
+                assert got[r].tobytes() == want_ar[r].tobytes(), (world, rings, r, dt, op, count, red_bytes, "in place")
+        assert counts == sorted(counts, reverse=True), counts
+        # the whole round in one launch: at most one launch per round and rank
+        assert counts[-1] <= world * (world - 1)
+
+
+def test_coalesce_lists_one_range_per_ring():
+    """pg_plan_coalesce on one round of a two-ring plan: the segments of each
+    ring over consecutive transport groups are neighbours, so the round's
+    reduce steps become at most one range per ring, covering every element once."""
+    world, count, dt, es = 4, 40000, 1, 8
+    plan = pgamd.plan_reduce_scatter(1, world, count, dt, 1024, 0, 2, rings=2)
+    for k in range(world - 1):
+        steps = [s for s in plan if s["round"] == k and s["red_elems"]]
+        assert len(steps) > 8
+        ranges = pgamd.plan_coalesce(list(reversed(steps)), es)          # any order in
+        # one range per ring; a single one where the two rings' parts happen to be
+        # neighbours in both operands (at W = 4 both rings fold the same block in rounds 0 and 2)
+        assert len(ranges) == (2 if k == 1 else 1)
+        assert sum(g["elems"] for g in ranges) == sum(s["red_elems"] for s in steps)
+        for g in ranges:
+            mine = [s for s in steps if g["dst_off"] <= s["red_dst_off"] < g["dst_off"] + g["elems"] * es
+                    and s["red_dst_buf"] == g["dst_buf"]]
+            assert sum(s["red_elems"] for s in mine) == g["elems"]
+            assert {s["red_rev"] for s in mine} == {g["rev"]}
+    assert pgamd.plan_coalesce([], es) == []
