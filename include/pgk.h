@@ -52,7 +52,7 @@ PG_API int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int
 /* Up to 8 independent ranges in one launch: outs[j][i] = as[j][i] op bs[j][i]
  * for i < ns[j] (out may equal a or b within a range; ranges must not overlap
  * each other).  Same numerics as pgk_reduce.  The ring executor reduces every
- * ring's arrived segments of a batch with one call.  start_event/stop_event
+ * ring's arrived segments with one call.  start_event/stop_event
  * (hipEvent_t as void*, may be NULL) receive the kernel's own begin/end
  * timestamps as in pgk_reduce_timed; ranges that cannot share one launch
  * (not 16-byte congruent) are launched one by one, stamped first-to-last. */

@@ -112,9 +112,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(T* __restrict__ out,
 // Several independent ranges in one launch: range j covers blocks
 // [first[j], first[j+1]) of the grid and computes out[j] = a[j] op b[j] with
 // the same body as k_reduce_vec.  One launch instead of one per range: the
-// ring executor reduces every ring's arrived segments of a batch at once
-// (they lie in different blocks of the buffers), so the launch ramp and tail
-// are paid once per batch, not once per ring.
+// ring executor reduces every ring's arrived segments at once (they lie in
+// different blocks of the buffers), so the launch ramp and tail are paid once
+// per launch, not once per ring.
 constexpr int kMaxRanges = 8;
 template <typename T>
 struct RangeList {
