@@ -150,3 +150,34 @@ def test_staged_all_reduce_captured_in_hip_graph(gpu, lib, oracle):
         for r in range(3):
             assert got[r].tobytes() == ref[r].tobytes(), (rep, r, "eager between replays")
         state = [oracle.fill(count, dt, op, 33000 + 10 * rep + r) for r in range(world)]
+
+
+def test_staged_all_reduce_special_values_match_existing_entry_point(gpu, lib, oracle):
+    """NaNs with payloads, infinities, signed zeros, denormals and DBL_MAX
+    scattered through every rank's input, sum and product, 1-4 rings: the bits
+    (NaN payloads included: both entry points fold every block in the same
+    order, the arrival on the left) equal pgx_sim_run's, and the int32
+    wrap cases equal the oracle's."""
+    rng = np.random.default_rng(99)
+    specials = np.array([0x7FF8000000000001, 0xFFF800000000BEEF, 0x7FF0000000000000, 0xFFF0000000000000,
+                         0x0000000000000000, 0x8000000000000000, 0x0000000000000001, 0x800FFFFFFFFFFFFF,
+                         0x7FEFFFFFFFFFFFFF, 0xFFEFFFFFFFFFFFFF, 0x3FF0000000000000, 0xBFF0000000000000], dtype=np.uint64)
+    for world, count, rings in ((4, 4099, 2), (8, 1001, 4), (3, 77, 1), (5, 300, 3)):
+        for op in (0, 1):
+            xs = []
+            for r in range(world):
+                x = oracle.fill(count, 1, op, 41000 + r).view(np.uint64).copy()
+                where = rng.random(count) < 0.3
+                x[where] = rng.choice(specials, int(where.sum()))
+                xs.append(x.view(np.float64))
+            got = _staged(lib, gpu, xs, count, 1, op, rings, True)
+            ref = _existing(lib, gpu, xs, count, 1, op, rings, True)
+            for r in range(world):
+                assert got[r].tobytes() == ref[r].tobytes(), (world, count, rings, op, r)
+    big = np.array([2**31 - 1, -2**31, 65536, -123456789, 987654, 1, -1, 0] * 64, dtype=np.int32)
+    xs = [np.roll(big, 3 * r).copy() for r in range(4)]
+    for op in (0, 1):
+        got = _staged(lib, gpu, xs, big.size, 0, op, 2, False)
+        want = oracle.ring_all_reduce(xs, 0, op, 2)
+        for r in range(4):
+            assert got[r].tobytes() == want[r].tobytes(), (op, r)
