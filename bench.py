@@ -75,12 +75,19 @@ def parse():
     ap.add_argument("--time-budget", type=float, default=480.0,
                     help="seconds since start after which no further optional leg is started (it is recorded as "
                          "skipped instead); the primary line always prints.  The driver gives one run 600 s")
+    ap.add_argument("--preflight", default=None, metavar="TRANSPORTS",
+                    help="(internal) child mode: two small checked calls per listed transport, nothing else; "
+                         "at N > 1 every rank starts one such child before it touches the GPU itself")
+    ap.add_argument("--no-preflight", action="store_true",
+                    help="skip the ring legs' preflight children (N > 1)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe-inclusive) leg")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 64 MiB .. 1 GiB kernel size table")
     return ap.parse_args()
 
 
-def dist_setup(args):
+def rank_setup(args):
+    """Rank, world size and this rank's device number from the launcher's
+    environment.  Touches no GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -96,12 +103,15 @@ def dist_setup(args):
         os.environ["NCCL_HOSTID"] = f"pg-bench-rehearsal-rank{rank}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
-    torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def dist_setup(rank, world):
+    """The control plane: gloo over CPU tensors only.  Touches no GPU."""
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
-    return rank, world, local
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
 _T0 = time.perf_counter()
@@ -932,6 +942,136 @@ def _link_probe(lib, h, rank, world, nbytes=256 << 20, reps=5):
     return out
 
 
+_PORT_OFFSET = {"rccl": 17, "xgmi": 19, "xgmi_push": 21, "xgmi_read": 23}
+
+
+def _transport_env(transport, rank, world, port_shift=0):
+    """Point the library's environment at one ring-leg transport; returns the
+    server list for connect_process_group."""
+    os.environ["PG_RANK"] = str(rank)
+    os.environ["PG_TRANSPORT"] = "xgmi" if transport.startswith("xgmi") else transport
+    os.environ["PG_XGMI_MODE"] = {"xgmi_push": "push", "xgmi_read": "read"}.get(transport, "auto")
+    os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + _PORT_OFFSET[transport] + port_shift)
+    return " ".join(["127.0.0.1"] * world).encode()
+
+
+# ---------------------------------------------------------------------------
+# Preflight: the first exchange of every transport happens in a child process.
+# A run on a node is the first time a rank's kernel reads (or writes) memory of
+# another DEVICE; if that faulted inside the measuring process, the fault would
+# end it and every rank with it, and the primary line would never print.  So
+# each rank, BEFORE it touches the GPU itself (a process that has initialised
+# the GPU starts no other program here), starts one child that makes two small
+# checked calls per transport (4 KiB: the one-shot path; 8 MiB: the large
+# path), reduce-scatter and all-reduce; the children are gone before the
+# parents' first HIP call, and only transports whose children all finished
+# clean get a leg.
+PREFLIGHT_COUNTS = (512, 1 << 20)            # doubles
+PREFLIGHT_TIMEOUT_S = 90.0
+_PF_OK, _PF_NOT_REACHED, _PF_FAILED = 0, 1, 2
+
+
+def preflight_child(args):
+    """`bench.py --preflight a,b,c`: for each transport in turn print "start t",
+    connect, run the checked calls, close, print "ok t" ("bad t: why" on a wrong
+    result or an error return).  Exit 0 only if every transport was ok."""
+    rank, world, local = rank_setup(args)
+    torch.cuda.set_device(local)
+    lib = pgamd.load()
+    bad = 0
+    for transport in args.preflight.split(","):
+        print(f"start {transport}", flush=True)
+        hosts = _transport_env(transport, rank, world, port_shift=40)
+        why = None
+        h = ctypes.c_void_p()
+        if lib.connect_process_group(hosts, ctypes.byref(h)) != 0:
+            why = "connect_process_group: " + pgamd.last_error()
+        else:
+            for count in PREFLIGHT_COUNTS:
+                x = _pattern(count, rank, world, DT, OP)
+                off, ln = pgamd.block_range(count, world, rank)
+                out = torch.zeros(count, dtype=x.dtype, device="cuda")
+                torch.cuda.synchronize()
+                for name, fn, o, n in (("reduce_scatter", lib.pg_reduce_scatter, off, ln),
+                                       ("all_reduce", lib.pg_all_reduce, 0, count)):
+                    if fn(x.data_ptr(), out.data_ptr(), count, DT, OP, h) != 0:
+                        why = why or f"{name}({count}): {pgamd.last_error()}"
+                    elif not torch.equal(out[:n], _expected_block(count, o, n, world, DT, OP)):
+                        why = why or f"{name}({count}): wrong result"
+            lib.pg_close(h)
+        print(f"ok {transport}" if why is None else f"bad {transport}: {why}", flush=True)
+        bad += why is not None
+    return 1 if bad else 0
+
+
+def _run_preflight_child(transports, args):
+    """Start this rank's child for `transports` and read what it got through:
+    {transport: (code, detail)}.  The transport a child died in (signal, time
+    limit, error exit before its "ok"/"bad" line) counts as failed.  Only ever
+    called before this process has made its first GPU call."""
+    import subprocess
+    assert not torch.cuda.is_initialized(), "preflight children are started before the parent touches the GPU"
+    cmd = [sys.executable, str(pathlib.Path(__file__).resolve()), "--preflight", ",".join(transports),
+           "--gpus", str(args.gpus)]
+    try:
+        cp = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=PREFLIGHT_TIMEOUT_S,
+                            text=True, errors="replace")
+        lines, rc, err = cp.stdout.splitlines(), cp.returncode, cp.stderr
+    except subprocess.TimeoutExpired as e:      # subprocess.run has killed the child
+        raw = e.stdout or ""
+        lines = (raw.decode(errors="replace") if isinstance(raw, bytes) else raw).splitlines()
+        raw = e.stderr or ""
+        rc, err = "time limit", raw.decode(errors="replace") if isinstance(raw, bytes) else raw
+    return _read_preflight(transports, lines, rc, err)
+
+
+def _read_preflight(transports, lines, rc, err=""):
+    got = {t: (_PF_NOT_REACHED, "not reached") for t in transports}
+    running = None
+    for ln in lines:
+        word, _, rest = ln.partition(" ")
+        name = rest.split(":")[0]
+        if word == "start" and name in got:
+            running = name
+        elif word == "ok" and name in got:
+            got[name], running = (_PF_OK, "ok"), None
+        elif word == "bad" and name in got:
+            got[name], running = (_PF_FAILED, rest), None
+    if running is not None:
+        tail = [ln for ln in err.splitlines() if ln.strip()][-1:] or [""]
+        end = f"signal {-rc}" if isinstance(rc, int) and rc < 0 else f"exit {rc}"
+        got[running] = (_PF_FAILED, f"child ended in it ({end}): {tail[0][:200]}")
+    return got
+
+
+def preflight(args, rank, world, transports, run_child=_run_preflight_child):
+    """{transport: None (every rank's child finished it clean) | reason}.  The
+    ranks agree after each round of children (one max-reduce of the codes): the
+    transports before the first one that failed anywhere are settled, that one
+    is out, and the ones after it go to a fresh round of children, so one
+    transport's fault does not cost the others their legs."""
+    verdict, left = {}, list(transports)
+    while left:
+        got = run_child(left, args)
+        codes = [got[t][0] for t in left]
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor(codes, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            worst = [int(v) for v in t]
+        else:
+            worst = codes
+        cut = next((i for i, c in enumerate(worst) if c != _PF_OK), len(left))
+        for t in left[:cut]:
+            verdict[t] = None
+        if cut < len(left):
+            mine = got[left[cut]]
+            verdict[left[cut]] = ("preflight failed on some rank; this rank: " + mine[1]) if mine[0] != _PF_OK \
+                else "preflight failed on another rank (this rank's child finished it)"
+        left = left[cut + 1:]
+    return verdict
+
+
 def ring_leg(lib, args, rank, world, transport, sink):
     """pg_reduce_scatter across the ranks, device-resident, BASELINE configs 3-5.
     transport: "rccl" (P2P ring over xGMI) or "xgmi" (direct peer reads).
@@ -947,12 +1087,7 @@ def ring_leg(lib, args, rank, world, transport, sink):
         count //= args.ring_div
         cfg += f" / {args.ring_div} (rehearsal size)"
     es = pgamd.ELEM_SIZE[dt]
-    hosts = " ".join(["127.0.0.1"] * world).encode()
-    os.environ["PG_RANK"] = str(rank)
-    os.environ["PG_TRANSPORT"] = "xgmi" if transport.startswith("xgmi") else transport
-    os.environ["PG_XGMI_MODE"] = {"xgmi_push": "push", "xgmi_read": "read"}.get(transport, "auto")
-    os.environ["PG_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) +
-                                {"rccl": 17, "xgmi": 19, "xgmi_push": 21, "xgmi_read": 23}[transport])
+    hosts = _transport_env(transport, rank, world)
     core_only = transport in ("xgmi_push", "xgmi_read")    # the correctness probe and the timed call
     h = ctypes.c_void_p()
     progress(rank, f"  {transport}: connect_process_group")
@@ -1120,8 +1255,19 @@ def ring_leg(lib, args, rank, world, transport, sink):
 def main():
     global _BUDGET_S
     args = parse()
+    if args.preflight:
+        sys.exit(preflight_child(args))
     _BUDGET_S = args.time_budget if args.time_budget > 0 else None
-    rank, world, local = dist_setup(args)
+    rank, world, local = rank_setup(args)
+    dist_setup(rank, world)
+    # the ring legs' preflight children run now, while this process has not made
+    # a single GPU call (see "Preflight" above), and have ended before it does
+    pf = None
+    if world > 1 and not args.no_ring and not args.no_preflight:
+        progress(rank, "preflight children (two small checked calls per ring transport)")
+        with leg_clock("ring.preflight"):
+            pf = preflight(args, rank, world, args.transports.split(","))
+    torch.cuda.set_device(local)
     lib = pgamd.load()
     # the size table first: the primary measurement then starts on a GPU already at its streaming clocks
     sizes = None
@@ -1242,7 +1388,12 @@ def main():
         dog = threading.Timer(args.ring_timeout, _expire)
         dog.daemon = True
         dog.start()
+        if pf is not None and line is not None:
+            line["ring_preflight"] = {t: ("ok" if why is None else why) for t, why in pf.items()}
         for transport in args.transports.split(","):
+            if pf is not None and pf[transport] is not None:
+                ring[transport] = {"error": "no leg: " + pf[transport]}
+                continue
             if past_budget(world):           # the same answer on every rank
                 ring[transport] = {"skipped": "time budget"}
                 continue

@@ -178,3 +178,25 @@ def test_r03_sweeps_cover_both_schedules(world, key, knob):
         assert {row[k] for row in sw["rows"] if row[a] == algo} == values, algo
         assert sum(row[cols.index("is_default")] for row in sw["rows"] if row[a] == algo) == 1
     assert set(sw["by_algo"]) == {"ring", "direct"} and sw["truncated_by_time_budget"] is False
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_r03_rehearsals_ran_their_preflight(world):
+    """At N > 1 each rank's first exchange on every transport happens in a child
+    process before the measuring process touches the GPU; the line records what
+    the children found and how long they took."""
+    line = _line(f"r03_bench_n{world}_onegpu_rehearsal.json")
+    assert line["ring_preflight"] == {t: "ok" for t in ("xgmi", "xgmi_push", "xgmi_read", "rccl")}
+    assert 0 < line["elapsed_s"]["ring.preflight"] < 60
+
+
+def test_r03_refused_preflight_costs_only_that_transport():
+    """The same run with the xgmi reach check forced to fail (PG_XGMI_FAIL_REACH
+    = -1, no fault involved): the xgmi legs are recorded as not run, with the
+    child's reason, the rccl leg and the primary line are there as ever."""
+    line = _line("r03_bench_n2_preflight_refused.json")
+    pf = line["ring_preflight"]
+    assert pf["rccl"] == "ok" and "cannot map a peer's device memory" in pf["xgmi"]
+    assert line["ring"]["xgmi"]["error"].startswith("no leg: preflight failed")
+    assert line["ring"]["xgmi_push"]["error"].startswith("no leg: preflight failed")
+    assert line["ring"]["rccl"]["ok"] is True and line["value"] > 0

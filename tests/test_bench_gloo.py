@@ -105,3 +105,77 @@ def test_sweep_summary_names_the_fastest_row_per_schedule():
     assert s["direct"] == {"fastest": 16 << 20, "fastest_GBps": 25.0, "fastest_over_default": 1.25,
                            "in_ring_reduce_frac_at_default": 0.78}
     assert s["ring"]["fastest"] == 8 << 20 and s["ring"]["fastest_over_default"] == 1.1
+
+
+def test_preflight_reads_a_childs_output():
+    """What a preflight child printed decides each transport: ok, bad (with its
+    reason), the one it died in, and the ones it never reached."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    import bench
+    names = ["xgmi", "xgmi_push", "rccl"]
+    got = bench._read_preflight(names, ["start xgmi", "ok xgmi", "start xgmi_push", "ok xgmi_push", "start rccl",
+                                        "ok rccl"], 0)
+    assert [got[t][0] for t in names] == [bench._PF_OK] * 3
+    got = bench._read_preflight(names, ["start xgmi", "ok xgmi", "start xgmi_push"], -6,
+                                "warning\nMemory access fault by GPU node-2\n")
+    assert got["xgmi"][0] == bench._PF_OK and got["rccl"][0] == bench._PF_NOT_REACHED
+    assert got["xgmi_push"][0] == bench._PF_FAILED
+    assert "signal 6" in got["xgmi_push"][1] and "Memory access fault" in got["xgmi_push"][1]
+    got = bench._read_preflight(names, ["start xgmi", "bad xgmi: all_reduce(512): wrong result", "start xgmi_push",
+                                        "ok xgmi_push", "start rccl"], "time limit")
+    assert got["xgmi"] == (bench._PF_FAILED, "xgmi: all_reduce(512): wrong result")
+    assert got["xgmi_push"][0] == bench._PF_OK
+    assert got["rccl"][0] == bench._PF_FAILED and "time limit" in got["rccl"][1]
+    assert bench._read_preflight(names, [], 1)["xgmi"][0] == bench._PF_NOT_REACHED
+
+
+def _preflight_worker(rank, world, port, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        rounds = []
+
+        def child(left, args):
+            # rank 1's child dies inside xgmi_push (first round); everything else finishes clean
+            rounds.append(list(left))
+            lines = []
+            for t in left:
+                lines.append(f"start {t}")
+                if t == "xgmi_push" and rank == 1:
+                    return bench._read_preflight(left, lines, -6, "Memory access fault by GPU\n")
+                lines.append(f"ok {t}")
+            return bench._read_preflight(left, lines, 0)
+
+        names = ["xgmi", "xgmi_push", "xgmi_read", "rccl"]
+        verdict = bench.preflight(None, rank, world, names, run_child=child)
+        q.put((rank, verdict, rounds))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_preflight_ranks_agree_and_later_transports_get_a_fresh_round():
+    """One rank's child dies in the second transport: every rank drops exactly
+    that transport, keeps the one before it, and sends the ones after it to a
+    second round of children (where they pass)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preflight_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, verdict, rounds in res:
+        assert isinstance(verdict, dict), verdict
+        assert verdict["xgmi"] is None and verdict["xgmi_read"] is None and verdict["rccl"] is None
+        assert rounds == [["xgmi", "xgmi_push", "xgmi_read", "rccl"], ["xgmi_read", "rccl"]]
+    assert "signal 6" in res[1][1]["xgmi_push"] and "another rank" in res[0][1]["xgmi_push"]
