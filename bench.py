@@ -93,6 +93,15 @@ def rank_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    on_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > 1 and os.environ.get("PG_BENCH_ONE_GPU") != "1" and torch.cuda.device_count() < on_node:
+        # (device_count() initialises nothing, and every rank of the node gets the same
+        # answer.)  More ranks than GPUs: the run can only be the one-GPU rehearsal, at its
+        # sizes; the line says so instead of the launch failing
+        os.environ["PG_BENCH_ONE_GPU"] = "1"
+        os.environ["PG_BENCH_ONE_GPU_AUTO"] = "1"
+        if args.ring_div == 1:
+            args.ring_div = 4 if world <= 4 else 8
     if os.environ.get("PG_BENCH_ONE_GPU") == "1":   # rehearsal of the N>1 path on a 1-GPU box
         local = 0
         os.environ["PG_DEVICE"] = "0"
@@ -1352,6 +1361,10 @@ def main():
             "config1": cfg1,
             "ring": None,
             "kernel": lib.pgk_version().decode(),
+            "one_gpu_rehearsal": (None if os.environ.get("PG_BENCH_ONE_GPU") != "1" else
+                                  "every rank shares GPU 0" + (" (chosen by bench.py: fewer GPUs than ranks)"
+                                                               if os.environ.get("PG_BENCH_ONE_GPU_AUTO") else "")
+                                  + ": value, roofline and ring rates are not a node's"),
             "elapsed_s": _ELAPSED,       # per leg, filled in place; "total" is set just before printing
             "time_budget_s": _BUDGET_S,
         }

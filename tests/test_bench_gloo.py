@@ -179,3 +179,33 @@ def test_preflight_ranks_agree_and_later_transports_get_a_fresh_round():
         assert verdict["xgmi"] is None and verdict["xgmi_read"] is None and verdict["rccl"] is None
         assert rounds == [["xgmi", "xgmi_push", "xgmi_read", "rccl"], ["xgmi_read", "rccl"]]
     assert "signal 6" in res[1][1]["xgmi_push"] and "another rank" in res[0][1]["xgmi_push"]
+
+
+def test_more_ranks_than_gpus_becomes_the_one_gpu_rehearsal(monkeypatch):
+    """Launched with more ranks on the node than it has GPUs, every rank takes
+    the one-GPU rehearsal (device 0, per-rank RCCL host id, divided ring
+    shapes) instead of failing on a device that does not exist.  The decision
+    uses only the node's device count, so all ranks decide alike."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "rdma-ring-collectives_amd")]
+    import argparse
+    import bench
+    import torch
+    for k in ("PG_BENCH_ONE_GPU", "PG_BENCH_ONE_GPU_AUTO", "PG_DEVICE", "NCCL_HOSTID"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    for rank in (0, 3):
+        monkeypatch.setenv("WORLD_SIZE", "4")
+        monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+        monkeypatch.setenv("RANK", str(rank))
+        monkeypatch.setenv("LOCAL_RANK", str(rank))
+        monkeypatch.delenv("PG_BENCH_ONE_GPU", raising=False)
+        args = argparse.Namespace(gpus=4, ring_div=1)
+        assert bench.rank_setup(args) == (rank, 4, 0)
+        assert os.environ["PG_BENCH_ONE_GPU"] == "1" and os.environ["PG_DEVICE"] == "0"
+        assert os.environ["NCCL_HOSTID"].endswith(f"rank{rank}") and args.ring_div == 4
+    # enough GPUs: nothing changes
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    for k in ("PG_BENCH_ONE_GPU", "PG_BENCH_ONE_GPU_AUTO", "PG_DEVICE", "NCCL_HOSTID"):
+        monkeypatch.delenv(k, raising=False)
+    args = argparse.Namespace(gpus=4, ring_div=1)
+    assert bench.rank_setup(args) == (3, 4, 3) and "PG_BENCH_ONE_GPU" not in os.environ and args.ring_div == 1
