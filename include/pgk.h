@@ -38,13 +38,16 @@ extern "C" {
  * (reference src/pg.c:151-159): int32 wraps (two's complement), double is one
  * IEEE-754 add or multiply per element (round-to-nearest, denormals kept), so
  * results are bit-identical to the reference loop for every non-NaN result.
- * dst and src must not partially overlap (dst == src is allowed).
+ * dst == src is allowed; dst and src overlapping at different addresses is
+ * refused (-1): the reference loop's element-by-element order is not what a
+ * parallel launch would compute there.
  * n == 0 is a no-op returning 0.  dt/op outside the values above -> -1.
  * Above 512 MiB per operand the call is several back-to-back launches on
  * `stream` (each at most 512 MiB), which measure faster than one. */
 PG_API int pgk_reduce(void *dst, const void *src, size_t n, int dt, int op, void *stream);
 
-/* out[i] = a[i] op b[i] (out may equal a or b).  Same numerics as pgk_reduce;
+/* out[i] = a[i] op b[i] (out may equal a or b; any other overlap of out with
+ * an operand is refused).  Same numerics as pgk_reduce;
  * used where the ring must not modify the caller's send buffer. */
 PG_API int pgk_reduce_out(void *out, const void *a, const void *b, size_t n, int dt, int op,
                    void *stream);

@@ -468,12 +468,26 @@ hipError_t launch_t(T* out, const T* a, const T* b, size_t n, hipStream_t s, Tim
   return hipGetLastError();
 }
 
+// Two ranges of `bytes` that intersect without being the same range.
+inline bool partly_overlap(const void* p, const void* q, size_t bytes) {
+  const uintptr_t x = (uintptr_t)p, y = (uintptr_t)q;
+  return x != y && x < y + bytes && y < x + bytes;
+}
+
 int launch(void* out, const void* a, const void* b, size_t n, int dt, int op, void* stream,
            Timing tm = Timing{nullptr, nullptr}) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (n == 0) return 0;
   if (!out || !a || !b) { set_err("pgk: NULL buffer with n=%zu", n); return -1; }
+  // The reference loop runs element by element, so operands that overlap
+  // at different addresses see each other's results in index order there; a
+  // parallel launch cannot reproduce that, and says so instead of guessing.
+  const size_t bytes = n * (dt == PGK_DT_INT32 ? 4 : 8);
+  if (partly_overlap(out, a, bytes) || partly_overlap(out, b, bytes)) {
+    set_err("pgk: the output overlaps an operand at a different address (n=%zu)", n);
+    return -1;
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if (dt == PGK_DT_INT32) {

@@ -229,6 +229,20 @@ def test_invalid_arguments(gpu, lib):
     assert lib.pgk_reduce(ptr(t), ptr(t), 16, 0, 2, stream(torch)) == -1
     assert lib.pgk_reduce(ptr(t), None, 16, 0, 0, stream(torch)) == -1
     assert lib.pgk_reduce(ptr(t), ptr(t), 0, 0, 0, stream(torch)) == 0
+    # operands that overlap at different addresses: the reference's loop (src/pg.c:151-159)
+    # would feed results back in index order; refused, and nothing is written
+    u = torch.arange(32, dtype=torch.int32, device="cuda")
+    before = u.clone()
+    for dst_off, src_off in ((0, 4), (4, 0), (0, 60)):
+        assert lib.pgk_reduce(ptr(u) + dst_off, ptr(u) + src_off, 16, 0, 0, stream(torch)) == -1
+        assert b"overlaps an operand" in lib.pgk_last_error()
+    assert lib.pgk_reduce_out(ptr(u) + 8, ptr(u), ptr(u) + 64, 8, 0, 0, stream(torch)) == -1
+    torch.cuda.synchronize()
+    assert torch.equal(u, before)
+    # adjacent, not overlapping: fine
+    assert lib.pgk_reduce(ptr(u), ptr(u) + 64, 16, 0, 0, stream(torch)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(u[:16], before[:16] + before[16:])
 
 
 def test_reduce_host_staged(gpu, lib, oracle):
