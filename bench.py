@@ -454,9 +454,11 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
     rows = []
     dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
     VP = ctypes.c_void_p
-    for label, rng in (("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings", 64 << 20),
-                       ("one transport group: 4 MiB x 4 inflight", 16 << 20), ("32 MiB per source", 32 << 20),
-                       ("128 MiB per source", 128 << 20), ("one group of 1 MiB x 4", 4 << 20)):
+    for label, rng, burst in (("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings", 64 << 20, 1),
+                              ("the same, one tile per wave (burst form off)", 64 << 20, 0),
+                              ("one transport group: 4 MiB x 4 inflight", 16 << 20, 1),
+                              ("32 MiB per source", 32 << 20, 1), ("128 MiB per source", 128 << 20, 1),
+                              ("one group of 1 MiB x 4", 4 << 20, 1)):
         slot = max(64 << 20, rng)
         sets = SWEEP_POOL // (slot * (nsrc + 1))
 
@@ -466,15 +468,21 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
             if lib.pgk_reduce_multi_timed(b0 + slot * nsrc, srcs, nsrc, rng // 8, dt, op, sh, ev[0], ev[1]) != 0:
                 raise RuntimeError(pgamd.last_error())
 
-        ms, sms = _time_launches(launch, e0, e1, stamp, lib, world, reps)
+        lib.pgk_tune_fold(burst)
+        try:
+            ms, sms = _time_launches(launch, e0, e1, stamp, lib, world, reps)
+        finally:
+            lib.pgk_tune_fold(1)
         traffic = (nsrc + 1) * rng
         rows.append([label, nsrc, rng, round(ms * 1e3, 2),
                      round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), round(sms * 1e3, 2),
                      round(traffic / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)])
     return {"columns": ["launch", "sources", "bytes_per_source", "kernel_us", "frac", "stamped_us", "stamped_frac"],
             "rows": rows,
-            "note": "one pgk_reduce_multi launch = one direct-exchange fold of one ring part (W = 8 sources), "
-                    "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults"}
+            "note": "one pgk_reduce_multi call = one direct-exchange fold of one ring part (W = 8 sources), "
+                    "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults. "
+                    "From 32 MiB per source the call takes the burst form (launches of at most 64 MiB per source "
+                    "in which every wave folds all its tiles before it stores any); row 2 is row 1 without it"}
 
 
 def cpu_baseline(args):

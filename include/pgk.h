@@ -69,9 +69,19 @@ PG_API int pgk_reduce_ranges(void *const *outs, const void *const *as, const voi
 PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                      void *stream);
 /* The same launch with the kernel's own begin/end timestamps recorded into two
- * HIP events (as pgk_reduce_timed; NULL events = untimed). */
+ * HIP events (as pgk_reduce_timed; NULL events = untimed).
+ * From 5 to 8 sources and 32 MiB per source both calls take the burst form:
+ * launches of at most 64 MiB per source in which every wave folds all its
+ * tiles before it stores any (the chip reads, then writes), 80-82% of the HBM
+ * peak against 73-75% for one tile per wave; the events then stamp the first
+ * launch's begin and the last one's end.  out may be one of the sources. */
 PG_API int pgk_reduce_multi_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                                   void *stream, void *start_event, void *stop_event);
+/* The same fold, never in the burst form: for sources that are mostly peers'
+ * memory read over xGMI, where the links bound the rate and the burst form
+ * (tuned on local HBM) has not been measured. */
+PG_API int pgk_reduce_multi_remote_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
+                                         void *stream, void *start_event, void *stop_event);
 
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]
@@ -122,6 +132,10 @@ PG_API int pgk_synchronize(void);
  * 0 = default cache policy, <0 = keep.  Defaults are the measured best
  * on MI355X. */
 PG_API int pgk_tune(int blocks_per_cu, int nontemporal);
+
+/* burst: 1 = pgk_reduce_multi may take its burst form (default), 0 = never,
+ * <0 = keep.  Process-wide; results are bit-identical either way. */
+PG_API int pgk_tune_fold(int burst);
 
 /* Vector-kernel shape: threads per block x 16-byte vectors per operand each
  * thread keeps in flight.  Instantiated: 256x2, 256x4, 256x8, 512x2, 1024x1;

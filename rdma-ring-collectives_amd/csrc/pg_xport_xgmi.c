@@ -699,9 +699,11 @@ static int finish(struct pg *pg, int zero_copy, int fail) {
 
 /* out = fold over ranks of this rank's block (at off_elems, len elements),
  * each ring part in its ring's order (include/pg_ext.h): bit-identical to the
- * P2P ring with the same PG_RINGS. */
+ * P2P ring with the same PG_RINGS.  local_sources: every by_rank[] is this
+ * GPU's own memory (push mode), so the fold may take the form tuned for local
+ * HBM; peers' memory read over the links keeps the plain streaming form. */
 static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size_t off_elems, size_t len, int dt,
-                      int op) {
+                      int op, int local_sources) {
   struct pg_impl *im = (struct pg_impl *)pg->impl;
   if (!len) return 0;
   int W = pg->world_size, r = pg->rank;
@@ -738,7 +740,8 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
       if (pg_kt_pair(im, &t0, &t1)) return -1;
       im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * pl * es);
     }
-    if (pgk_reduce_multi_timed((char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red, t0, t1)) {
+    if ((local_sources ? pgk_reduce_multi_timed : pgk_reduce_multi_remote_timed)(
+            (char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red, t0, t1)) {
       pg_set_error("xgmi: %s", pgk_last_error());
       return -1;
     }
@@ -858,7 +861,7 @@ static int rs_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int d
     if (pg_ensure(&im->dout, &im->dout_cap, len * es)) fail = 1;   /* reported by finish() on every rank */
     out = im->dout;
   }
-  if (!fail && fold_block(pg, out, by_rank, fold_off, len, dt, op)) fail = 1;
+  if (!fail && fold_block(pg, out, by_rank, fold_off, len, dt, op, pushed)) fail = 1;
   int fin = finish(pg, zc, fail);
   if (fin) return fin;
   if (!rd && len && pg_copy_parallel(recvbuf, out, len * es)) return -1;
@@ -954,7 +957,7 @@ static int ar_once(struct pg *pg, void *sendbuf, void *recvbuf, int count, int d
   } else {
     /* my block of the result goes to R[which] so that every rank can gather it */
     if (ensure(pg, XG_REG_R, bytes)) return -1;
-    if (!fail && fold_block(pg, slot(x, XG_REG_R, pg->rank, which) + off * es, by_rank, fold_off, len, dt, op))
+    if (!fail && fold_block(pg, slot(x, XG_REG_R, pg->rank, which) + off * es, by_rank, fold_off, len, dt, op, 0))
       fail = 1;
     double tb = us_now();
     if (barrier(pg)) return -1;

@@ -204,6 +204,68 @@ __global__ __launch_bounds__(kMultiVecBlock) void k_reduce_multi_vec(T* __restri
   }
 }
 
+// The same fold with its stores gathered into one burst per launch.  HBM
+// serves a thin stream of writes spread through many read streams badly: the
+// fold above, one tile per wave and a store right behind its loads, streams
+// at 73-75% of the peak from five sources up, where its reads alone reach 85-88%
+// (tools/lab/run_mix_lab.py: the same bytes written cost 0.17 us per MiB as a
+// dense stream and 0.46 us per MiB spread through eight read streams).  Here
+// every wave folds U tiles into registers, reads only, and stores its U results
+// at the end; the grid is one-shot and every workgroup is resident at once (at
+// most 512 workgroups at U = 32: two per CU at its 236 VGPRs), so the chip
+// reads for most of the launch and then writes: 80-82% at 5-8 sources x 64 MiB
+// (tools/lab/run_burst_lab2.py).  A launch covers at most kBurstPieceBytes per
+// source (what the resident waves' registers hold); larger calls are several
+// launches.  It does not pay below five sources or 32 MiB per source.
+// A lane reads its elements of every source before it writes them, so out may
+// be one of the sources, as in the kernel above.
+constexpr int kBurstBlock = 256;
+constexpr int kBurstBlocks = 512;                  // workgroups per full-size launch
+constexpr int kBurstMaxU = 32;
+constexpr size_t kBurstMinBytes = 32u << 20;       // per source, whole call
+constexpr size_t kBurstPieceBytes = (size_t)kBurstBlocks * kBurstBlock * kBurstMaxU * 16;   // 64 MiB
+
+template <typename T, int OP, int NS, int U>
+__global__ __launch_bounds__(kBurstBlock) void k_reduce_multi_burst(T* __restrict__ out, SrcList<T> src,
+                                                                    unsigned head, size_t v0, size_t v1,
+                                                                    unsigned edge_head, unsigned edge_tail,
+                                                                    size_t tail_e) {
+  using V = typename VecOf<T>::type;
+  // the call's unaligned edge elements, on its first launch only
+  if (blockIdx.x == 0 && threadIdx.x < edge_head + edge_tail) {
+    const size_t e = threadIdx.x < edge_head ? threadIdx.x : tail_e + (threadIdx.x - edge_head);
+    T acc = src.p[0][e];
+#pragma unroll
+    for (int j = 1; j < NS; ++j) acc = apply<OP>(acc, src.p[j][e]);
+    out[e] = acc;
+  }
+  const V* vs[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) vs[j] = reinterpret_cast<const V*>(src.p[j] + head);
+  V* vo = reinterpret_cast<V*>(out + head);
+  const size_t base = v0 + (size_t)blockIdx.x * (kBurstBlock * U) + threadIdx.x;
+  V r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t i = base + (size_t)u * kBurstBlock;
+    if (i < v1) {
+      V x[NS];
+#pragma unroll
+      for (int j = 0; j < NS; ++j) x[j] = ld<true>(vs[j] + i);
+      V acc = x[0];
+#pragma unroll
+      for (int j = 1; j < NS; ++j) acc = apply<OP>(acc, x[j]);
+      r[u] = acc;
+    }
+  }
+  asm volatile("" ::: "memory");         // no store is scheduled among the loads
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t i = base + (size_t)u * kBurstBlock;
+    if (i < v1) st<true>(vo + i, r[u]);
+  }
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kMultiBlock) void k_reduce_multi_scalar(T* __restrict__ out, SrcList<T> src,
                                                                      int nsrc, size_t n) {
@@ -319,6 +381,7 @@ void set_err(const char* fmt, ...) {
 // Tuning (process-wide).  The defaults are the measured best on MI355X (the figures are beside each knob).
 int g_blocks_per_cu = 0;   // one-shot grid: 6403 vs 6200 GB/s capped at 8/CU (sweep r01)
 int g_nontemporal = 1;
+int g_fold_burst = 1;          // pgk_tune_fold
 // Vector shape: 0x0 = by size (shape_for); else forced by pgk_tune_shape.
 int g_block = 0;
 int g_unroll = 0;
@@ -563,8 +626,59 @@ hipError_t launch_ranges_t(T* const* outs, const T* const* as, const T* const* b
   return hipGetLastError();
 }
 
+template <typename T, int OP, int NS>
+void launch_burst_u(int u, unsigned grid, T* out, const SrcList<T>& sl, unsigned head, size_t v0, size_t v1,
+                    unsigned eh, unsigned et, size_t tail_e, hipStream_t s, Timing tm) {
+#define PGK_BURST_CASE(U) \
+  hipExtLaunchKernelGGL((k_reduce_multi_burst<T, OP, NS, U>), dim3(grid), dim3(kBurstBlock), 0, s, tm.start, tm.stop, \
+                        0, out, sl, head, v0, v1, eh, et, tail_e)
+  if (u <= 16) PGK_BURST_CASE(16);
+  else PGK_BURST_CASE(32);
+#undef PGK_BURST_CASE
+}
+
+// The burst fold of a whole call (5 <= nsrc <= 8, nvec * 16 >= kBurstMinBytes).
+// The form needs the chip full: launches of exactly kBurstPieceBytes per source
+// (512 workgroups, two per CU, 32 tiles per wave) reach 82-84%, a launch of 288
+// workgroups 65%.  So the call is cut into full launches; a rest of 32 MiB or
+// more is one launch of 16 tiles per wave (512 .. 1023 workgroups, four per CU
+// fit); a smaller rest is returned to the caller (`done` = vectors covered),
+// which folds it one tile per wave.  The first launch also folds the call's
+// unaligned edge elements.
 template <typename T, int OP>
-hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s, Timing tm) {
+hipError_t launch_burst(T* out, const SrcList<T>& sl, int nsrc, unsigned head, size_t nvec, unsigned tail,
+                        hipStream_t s, Timing tm, size_t* done) {
+  const size_t full = kBurstPieceBytes / 16;                               // vectors per full-size launch
+  const size_t rest_min = kBurstMinBytes / 16;
+  const size_t tail_e = head + nvec * (16 / sizeof(T));
+  size_t v0 = 0;
+  while (v0 < nvec) {
+    const size_t left = nvec - v0;
+    int u;
+    size_t v1;
+    if (left >= full) { u = 32; v1 = v0 + full; }
+    else if (left >= rest_min) { u = 16; v1 = nvec; }
+    else break;
+    const unsigned grid = (unsigned)((v1 - v0 + (size_t)kBurstBlock * u - 1) / ((size_t)kBurstBlock * u));
+    const Timing tq{v0 == 0 ? tm.start : nullptr, v1 == nvec ? tm.stop : nullptr};
+    const unsigned eh = v0 == 0 ? head : 0, et = v0 == 0 ? tail : 0;
+    switch (nsrc) {
+      case 5: launch_burst_u<T, OP, 5>(u, grid, out, sl, head, v0, v1, eh, et, tail_e, s, tq); break;
+      case 6: launch_burst_u<T, OP, 6>(u, grid, out, sl, head, v0, v1, eh, et, tail_e, s, tq); break;
+      case 7: launch_burst_u<T, OP, 7>(u, grid, out, sl, head, v0, v1, eh, et, tail_e, s, tq); break;
+      default: launch_burst_u<T, OP, 8>(u, grid, out, sl, head, v0, v1, eh, et, tail_e, s, tq);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    v0 = v1;
+  }
+  *done = v0;
+  return hipSuccess;
+}
+
+template <typename T, int OP>
+hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s, Timing tm,
+                          bool local_sources = true) {
   SrcList<T> sl{};
   uintptr_t m = (uintptr_t)out & 15;
   bool congruent = (m % sizeof(T)) == 0;
@@ -577,6 +691,17 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
     size_t head = m ? (16 - m) / sizeof(T) : 0;
     if (head > n) head = n;
     size_t nvec = (n - head) / W, tail = (n - head) % W;
+    if (local_sources && g_fold_burst && nsrc >= 5 && nsrc <= 8 && nvec * 16 >= kBurstMinBytes) {
+      size_t done = 0;
+      hipError_t e = launch_burst<T, OP>(out, sl, nsrc, (unsigned)head, nvec, (unsigned)tail, s, tm, &done);
+      if (e != hipSuccess || done == nvec) return e;
+      // the rest (under 32 MiB per source): one tile per wave, behind the bursts on the same stream
+      out += head + done * W;
+      for (int j = 0; j < nsrc; ++j) sl.p[j] += head + done * W;
+      nvec -= done;
+      head = tail = 0;
+      tm.start = nullptr;
+    }
     size_t g = (nvec + kMultiVecBlock - 1) / kMultiVecBlock;
     if (g == 0) g = 1;
     if (g > grid_cap(kMultiVecBlock)) g = grid_cap(kMultiVecBlock);
@@ -650,8 +775,8 @@ void launch_fold_bcast(void* const* outs, int nout, const unsigned char* area, s
 
 extern "C" {
 
-int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
-                           void* start_event, void* stop_event) {
+static int reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
+                        void* start_event, void* stop_event, bool local) {
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
@@ -664,15 +789,25 @@ int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t 
   hipError_t e;
   if (dt == PGK_DT_INT32) {
     const uint32_t* const* x = (const uint32_t* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s, tm)
-                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s, tm);
+    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s, tm, local)
+                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s, tm, local);
   } else {
     const double* const* x = (const double* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s, tm)
-                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s, tm);
+    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s, tm, local)
+                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s, tm, local);
   }
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
   return 0;
+}
+
+int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
+                           void* start_event, void* stop_event) {
+  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, true);
+}
+
+int pgk_reduce_multi_remote_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op,
+                                  void* stream, void* start_event, void* stop_event) {
+  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, false);
 }
 
 
@@ -911,6 +1046,11 @@ int pgk_synchronize(void) {
 int pgk_tune(int blocks_per_cu, int nontemporal) {
   if (blocks_per_cu >= 0) g_blocks_per_cu = blocks_per_cu;
   if (nontemporal >= 0) g_nontemporal = nontemporal ? 1 : 0;
+  return 0;
+}
+
+int pgk_tune_fold(int burst) {
+  if (burst >= 0) g_fold_burst = burst ? 1 : 0;
   return 0;
 }
 

@@ -115,6 +115,8 @@ _SIGS = {
     "pgk_reduce_ranges": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ),
                                _I, _I, _I, _VP, _VP, _VP]),
     "pgk_reduce_multi_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
+    "pgk_reduce_multi_remote_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
+    "pgk_tune_fold": (_I, [_I]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),

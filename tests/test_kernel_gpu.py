@@ -322,6 +322,70 @@ def test_reduce_multi_fold_order(gpu, lib, oracle, dt, op):
     assert lib.pgk_reduce_multi(ptr(out), srcs, 0, 4, dt, op, stream(torch)) == -1
 
 
+@pytest.mark.parametrize("nsrc,dt,op,nbytes,extra,shift,inplace", [
+    (5, 1, 0, 32 << 20, 0, 0, None),        # one launch of 16 tiles per wave
+    (8, 1, 0, 72 << 20, 5, 1, None),        # a full launch, a rest under 32 MiB (one tile per wave), ragged edges
+    (6, 0, 1, 100 << 20, 3, 3, None),       # a full launch and a rest of 36 MiB (16 tiles per wave), int32 product
+    (7, 0, 0, 130 << 20, 0, 0, None),       # two full launches and a 2 MiB rest
+    (8, 1, 1, 64 << 20, 0, 0, 7),           # in place over the last source (the ring's own block)
+    (5, 1, 0, 40 << 20, 2, 0, 0),           # in place over the first source
+])
+def test_reduce_multi_burst_form(gpu, lib, oracle, nsrc, dt, op, nbytes, extra, shift, inplace):
+    """From 5 sources and 32 MiB per source pgk_reduce_multi gathers its stores
+    into one burst per launch (launches of at most 64 MiB per source).  Same
+    left-to-right fold as nsrc-1 successive reduce_inplace steps (src/pg.c:151-159),
+    bit for bit; equal to the one-tile-per-wave form (pgk_tune_fold(0)) and to
+    the form for remote sources, byte for byte; stamped by its events."""
+    import ctypes
+    torch = gpu
+    es = 4 if dt == 0 else 8
+    n = nbytes // es + extra
+    xs = [oracle.fill(n + 4, dt, op, 4100 + 17 * nsrc + j) for j in range(nsrc)]
+    want = xs[0][shift:shift + n].copy()
+    for j in range(1, nsrc):
+        want = oracle.reduce(want, xs[j][shift:shift + n], dt, op)
+    D = [to_dev(torch, x) for x in xs]
+    srcs = (ctypes.c_void_p * nsrc)(*[ptr(d) + shift * es for d in D])
+    if inplace is None:
+        out = torch.zeros(n + 4, dtype=D[0].dtype, device="cuda")
+        ev = (ctypes.c_void_p(), ctypes.c_void_p())
+        assert lib.pgk_event_create(ctypes.byref(ev[0])) == 0 and lib.pgk_event_create(ctypes.byref(ev[1])) == 0
+        assert lib.pgk_reduce_multi_timed(ptr(out) + shift * es, srcs, nsrc, n, dt, op, stream(torch), ev[0], ev[1]) == 0
+        torch.cuda.synchronize()
+        ms = ctypes.c_float()
+        assert lib.pgk_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)) == 0
+        # first launch's begin to last launch's end: no faster than the HBM peak allows
+        assert ms.value * 1e-3 > (nsrc + 1) * n * es / 8e12
+        got = to_host(torch, out)
+        assert got[shift:shift + n].tobytes() == want.tobytes()
+        assert not got[:shift].any() and not got[shift + n:].any()           # nothing outside the range
+        for form in ("plain", "remote"):
+            other = torch.zeros(n + 4, dtype=D[0].dtype, device="cuda")
+            if form == "plain":
+                assert lib.pgk_tune_fold(0) == 0
+                try:
+                    assert lib.pgk_reduce_multi(ptr(other) + shift * es, srcs, nsrc, n, dt, op, stream(torch)) == 0
+                finally:
+                    lib.pgk_tune_fold(1)
+            else:
+                assert lib.pgk_reduce_multi_remote_timed(ptr(other) + shift * es, srcs, nsrc, n, dt, op, stream(torch),
+                                                         None, None) == 0
+            assert torch.equal(other, out), form
+            del other
+        lib.pgk_event_destroy(ev[0]), lib.pgk_event_destroy(ev[1])
+    else:
+        assert lib.pgk_reduce_multi(ptr(D[inplace]) + shift * es, srcs, nsrc, n, dt, op, stream(torch)) == 0
+        got = to_host(torch, D[inplace])
+        assert got[shift:shift + n].tobytes() == want.tobytes()
+        assert got[:shift].tobytes() == xs[inplace][:shift].tobytes()
+        assert got[shift + n:].tobytes() == xs[inplace][shift + n:].tobytes()
+        for j in range(nsrc):
+            if j != inplace:
+                assert to_host(torch, D[j]).tobytes() == xs[j].tobytes()      # the other sources untouched
+    del D
+    torch.cuda.empty_cache()
+
+
 def test_fold_blocks_and_gather(gpu, lib, oracle):
     """pgk_fold_blocks == the oracle's ring all-reduce (each block in its ring
     order); pgk_gather copies every range, 16-B and 4-B aligned forms."""
