@@ -17,24 +17,30 @@ import statistics
 import sys
 
 ROOT = pathlib.Path(__file__).resolve().parents[2]
-KERNEL = "k_reduce_multi_vec<double, 0, 8>"
+import re
+
+# the fold's two forms: one tile (one 16-B vector per work-item per source) per
+# wave, or the burst form with U vectors per work-item (from 32 MiB per source)
+FORMS = re.compile(r"k_reduce_multi_(vec<double, 0, 8>|burst<double, 0, 8, (\d+)>)")
 
 
 def summary(fetch_dir, write_dir):
     def rows(d, name):
         out = {}
         for r in csv.DictReader(open(pathlib.Path(d) / "run_counter_collection.csv")):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name:
-                out.setdefault(int(r["Grid_Size"]), []).append(float(r["Counter_Value"]))
+            m = FORMS.search(r["Kernel_Name"])
+            if m and r["Counter_Name"] == name:
+                per_item = int(m.group(2)) if m.group(2) else 1
+                out.setdefault((m.group(0), int(r["Grid_Size"]) * 16 * per_item), []).append(float(r["Counter_Value"]))
         return out
     f, w = rows(fetch_dir, "FETCH_SIZE"), rows(write_dir, "WRITE_SIZE")
     res = []
-    for grid in sorted(f):
-        size = grid * 16                      # one 16-B vector per work-item per source
-        hbm = (2 * statistics.median(f[grid]) + statistics.median(w[grid])) * 1024
-        res.append({"kernel": KERNEL, "MiB_per_source": size >> 20, "launches": [len(f[grid]), len(w[grid])],
-                    "FETCH_SIZE_KiB_median": statistics.median(f[grid]),
-                    "WRITE_SIZE_KiB_median": statistics.median(w[grid]),
+    for kernel, size in sorted(f, key=lambda t: t[1]):
+        key = (kernel, size)
+        hbm = (2 * statistics.median(f[key]) + statistics.median(w[key])) * 1024
+        res.append({"kernel": kernel, "MiB_per_source": size >> 20, "launches": [len(f[key]), len(w[key])],
+                    "FETCH_SIZE_KiB_median": statistics.median(f[key]),
+                    "WRITE_SIZE_KiB_median": statistics.median(w[key]),
                     "hbm_bytes_per_launch": round(hbm), "algorithmic_bytes_per_launch": 9 * size,
                     "hbm_over_algorithmic": round(hbm / (9 * size), 4)})
     print(json.dumps(res, indent=1))
@@ -55,7 +61,7 @@ sh = torch.cuda.current_stream().cuda_stream
 POOL = 4 << 30
 pool = torch.empty(POOL // 8, dtype=torch.float64, device="cuda").uniform_(-1, 1)
 VP = ctypes.c_void_p
-for mib in [int(a) for a in sys.argv[1:]] or [16, 64]:
+for mib in [int(a) for a in sys.argv[1:]] or [16, 32, 64]:
     size = mib << 20
     sets = POOL // (9 * size)
     for k in range(12):
