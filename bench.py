@@ -454,18 +454,21 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
     rows = []
     dt, op = pgamd.DT_DOUBLE, pgamd.OP_SUM
     VP = ctypes.c_void_p
-    for label, rng, burst in (("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings", 64 << 20, 1),
-                              ("the same, one tile per wave (burst form off)", 64 << 20, 0),
-                              ("one transport group: 4 MiB x 4 inflight", 16 << 20, 1),
-                              ("32 MiB per source", 32 << 20, 1), ("128 MiB per source", 128 << 20, 1),
-                              ("one group of 1 MiB x 4", 4 << 20, 1)):
+    for label, rng, burst, flags in (
+            ("defaults: PG_REDUCE_BYTES 128 MiB, 2 rings; the GPU to itself (the last flush of a call)", 64 << 20, 1, 0),
+            ("the same, one tile per wave (burst form off)", 64 << 20, 0, 0),
+            ("the same, PGK_FOLD_SHARED_GPU (the flushes that run beside transfers): two 32 MiB launches", 64 << 20, 1,
+             pgamd.FOLD_SHARED_GPU),
+            ("one transport group: 4 MiB x 4 inflight", 16 << 20, 1, 0),
+            ("32 MiB per source", 32 << 20, 1, 0), ("128 MiB per source", 128 << 20, 1, 0),
+            ("one group of 1 MiB x 4", 4 << 20, 1, 0)):
         slot = max(64 << 20, rng)
         sets = SWEEP_POOL // (slot * (nsrc + 1))
 
         def launch(i, ev=(None, None)):
             b0 = base + slot * (nsrc + 1) * (i % sets)
             srcs = (VP * nsrc)(*[b0 + slot * j for j in range(nsrc)])
-            if lib.pgk_reduce_multi_timed(b0 + slot * nsrc, srcs, nsrc, rng // 8, dt, op, sh, ev[0], ev[1]) != 0:
+            if lib.pgk_fold_timed(b0 + slot * nsrc, srcs, nsrc, rng // 8, dt, op, flags, sh, ev[0], ev[1]) != 0:
                 raise RuntimeError(pgamd.last_error())
 
         lib.pgk_tune_fold(burst)
@@ -482,7 +485,9 @@ def direct_batch_rows(lib, base, sh, e0, e1, stamp, rank, world, reps, nsrc=8):
             "note": "one pgk_reduce_multi call = one direct-exchange fold of one ring part (W = 8 sources), "
                     "(W+1) x bytes_per_source of traffic, double sum, local HBM sources; first row = the defaults. "
                     "From 32 MiB per source the call takes the burst form (launches of at most 64 MiB per source "
-                    "in which every wave folds all its tiles before it stores any); row 2 is row 1 without it"}
+                    "in which every wave folds all its tiles before it stores any); row 2 is row 1 without it, "
+                    "row 3 the form the direct exchange uses while transfers are still running (32 MiB launches "
+                    "that leave half of every CU's registers to the transport's kernels)"}
 
 
 def cpu_baseline(args):

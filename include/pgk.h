@@ -72,16 +72,26 @@ PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t
  * HIP events (as pgk_reduce_timed; NULL events = untimed).
  * From 5 to 8 sources and 32 MiB per source both calls take the burst form:
  * launches of at most 64 MiB per source in which every wave folds all its
- * tiles before it stores any (the chip reads, then writes), 80-82% of the HBM
+ * tiles before it stores any (the chip reads, then writes), 80-84% of the HBM
  * peak against 73-75% for one tile per wave; the events then stamp the first
  * launch's begin and the last one's end.  out may be one of the sources. */
 PG_API int pgk_reduce_multi_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                                   void *stream, void *start_event, void *stop_event);
-/* The same fold, never in the burst form: for sources that are mostly peers'
- * memory read over xGMI, where the links bound the rate and the burst form
- * (tuned on local HBM) has not been measured. */
-PG_API int pgk_reduce_multi_remote_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
-                                         void *stream, void *start_event, void *stop_event);
+/* pgk_reduce_multi_timed with what the caller knows about the launch:
+ *   PGK_FOLD_REMOTE_SOURCES  the sources are mostly peers' memory read over
+ *       xGMI: the links bound the rate, and the burst form (tuned on local HBM)
+ *       is not used;
+ *   PGK_FOLD_SHARED_GPU  other kernels (a transport's sends and receives) are
+ *       resident while the fold runs: the burst form is cut into 32 MiB
+ *       launches that use half of every CU's registers (79% of the peak, and
+ *       the same beside other kernels), where the 64 MiB launches of a fold
+ *       that has the GPU to itself (82-84%) fall to 69% beside eight foreign
+ *       workgroups.
+ * Same bits in every form.  Unknown flags -> -1. */
+#define PGK_FOLD_REMOTE_SOURCES 1u
+#define PGK_FOLD_SHARED_GPU 2u
+PG_API int pgk_fold_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op, unsigned flags,
+                          void *stream, void *start_event, void *stop_event);
 
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]

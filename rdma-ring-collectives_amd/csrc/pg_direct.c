@@ -171,7 +171,9 @@ static int direct_rs_core(struct pg *pg, const char *src, char *out, int count, 
             if (pg_kt_pair(im, &t0, &t1)) return -1;
             im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * (size_t)len * es);
           }
-          if (pgk_reduce_multi_timed(out + st[t].red_dst_off, srcs, W, (size_t)len, dt, op, (void *)im->red, t0, t1)) {
+          /* every flush but the last runs beside the next batches' transport kernels */
+          if (pgk_fold_timed(out + st[t].red_dst_off, srcs, W, (size_t)len, dt, op, j == n ? 0u : PGK_FOLD_SHARED_GPU,
+                             (void *)im->red, t0, t1)) {
             pg_set_error("direct: %s", pgk_last_error());
             return -1;
           }

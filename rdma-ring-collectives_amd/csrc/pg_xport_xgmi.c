@@ -740,8 +740,8 @@ static int fold_block(struct pg *pg, void *out, const char *const *by_rank, size
       if (pg_kt_pair(im, &t0, &t1)) return -1;
       im->stats.red_kernel_bytes += (int64_t)((size_t)(W + 1) * pl * es);
     }
-    if ((local_sources ? pgk_reduce_multi_timed : pgk_reduce_multi_remote_timed)(
-            (char *)out + po * es, srcs, W, pl, dt, op, (void *)im->red, t0, t1)) {
+    if (pgk_fold_timed((char *)out + po * es, srcs, W, pl, dt, op, local_sources ? 0u : PGK_FOLD_REMOTE_SOURCES,
+                       (void *)im->red, t0, t1)) {
       pg_set_error("xgmi: %s", pgk_last_error());
       return -1;
     }

@@ -211,19 +211,31 @@ __global__ __launch_bounds__(kMultiVecBlock) void k_reduce_multi_vec(T* __restri
 // (tools/lab/run_mix_lab.py: the same bytes written cost 0.17 us per MiB as a
 // dense stream and 0.46 us per MiB spread through eight read streams).  Here
 // every wave folds U tiles into registers, reads only, and stores its U results
-// at the end; the grid is one-shot and every workgroup is resident at once (at
-// most 512 workgroups at U = 32: two per CU at its 236 VGPRs), so the chip
-// reads for most of the launch and then writes: 80-82% at 5-8 sources x 64 MiB
-// (tools/lab/run_burst_lab2.py).  A launch covers at most kBurstPieceBytes per
-// source (what the resident waves' registers hold); larger calls are several
-// launches.  It does not pay below five sources or 32 MiB per source.
+// at the end; the grid is one-shot and every workgroup is resident at once, so
+// the chip reads for most of the launch and then writes.  What a launch may
+// hold is what the resident waves' registers hold, and the form only works
+// with a whole number of workgroups per CU, all of them resident from the
+// start (a launch of 576 or 640 workgroups runs at 64-76%; workgroups that
+// must wait for a free CU run as a second round behind the first):
+//   512 workgroups x 32 tiles (64 MiB per source; two per CU at ~220 VGPRs, a
+//       CU's whole register file): 82-84% on a GPU the fold has to itself,
+//       69% as soon as eight workgroups of another kernel are resident;
+//   768 x 16 (48 MiB; three per CU at ~124 VGPRs): 80-81%;
+//   512 x 16 (32 MiB; two per CU, half the register file): 79%, and the same
+//       beside 128 resident workgroups of 256 lanes x 128 VGPRs; it also fits
+//       beside waves of 256 VGPRs, which RCCL's kernels are
+// (tools/lab/burst_occupied_probe2.py).  So a fold that has the GPU to itself
+// is cut into 64 MiB launches, and one that runs beside communication kernels
+// (PGK_FOLD_SHARED_GPU) into 32 MiB ones.  It does not pay below five sources
+// or 32 MiB per source.
 // A lane reads its elements of every source before it writes them, so out may
 // be one of the sources, as in the kernel above.
 constexpr int kBurstBlock = 256;
-constexpr int kBurstBlocks = 512;                  // workgroups per full-size launch
-constexpr int kBurstMaxU = 32;
+constexpr int kBurstBlocks = 512;                  // workgroups per launch: two per CU
 constexpr size_t kBurstMinBytes = 32u << 20;       // per source, whole call
-constexpr size_t kBurstPieceBytes = (size_t)kBurstBlocks * kBurstBlock * kBurstMaxU * 16;   // 64 MiB
+constexpr size_t kBurstVecs32 = (size_t)kBurstBlocks * kBurstBlock * 32;       // 64 MiB per source
+constexpr size_t kBurstVecs16x3 = (size_t)kBurstBlocks / 2 * 3 * kBurstBlock * 16;   // 48 MiB, three per CU
+constexpr size_t kBurstVecs16 = (size_t)kBurstBlocks * kBurstBlock * 16;       // 32 MiB
 
 template <typename T, int OP, int NS, int U>
 __global__ __launch_bounds__(kBurstBlock) void k_reduce_multi_burst(T* __restrict__ out, SrcList<T> src,
@@ -637,29 +649,25 @@ void launch_burst_u(int u, unsigned grid, T* out, const SrcList<T>& sl, unsigned
 #undef PGK_BURST_CASE
 }
 
-// The burst fold of a whole call (5 <= nsrc <= 8, nvec * 16 >= kBurstMinBytes).
-// The form needs the chip full: launches of exactly kBurstPieceBytes per source
-// (512 workgroups, two per CU, 32 tiles per wave) reach 82-84%, a launch of 288
-// workgroups 65%.  So the call is cut into full launches; a rest of 32 MiB or
-// more is one launch of 16 tiles per wave (512 .. 1023 workgroups, four per CU
-// fit); a smaller rest is returned to the caller (`done` = vectors covered),
-// which folds it one tile per wave.  The first launch also folds the call's
-// unaligned edge elements.
+// The burst fold of a whole call (5 <= nsrc <= 8, nvec * 16 >= kBurstMinBytes),
+// as whole launches of the shapes above; what is left (under 32 MiB per source)
+// is returned to the caller (`done` = vectors covered), which folds it one tile
+// per wave.  The first launch also folds the call's unaligned edge elements.
 template <typename T, int OP>
 hipError_t launch_burst(T* out, const SrcList<T>& sl, int nsrc, unsigned head, size_t nvec, unsigned tail,
-                        hipStream_t s, Timing tm, size_t* done) {
-  const size_t full = kBurstPieceBytes / 16;                               // vectors per full-size launch
-  const size_t rest_min = kBurstMinBytes / 16;
+                        bool shared_gpu, hipStream_t s, Timing tm, size_t* done) {
   const size_t tail_e = head + nvec * (16 / sizeof(T));
   size_t v0 = 0;
   while (v0 < nvec) {
     const size_t left = nvec - v0;
     int u;
-    size_t v1;
-    if (left >= full) { u = 32; v1 = v0 + full; }
-    else if (left >= rest_min) { u = 16; v1 = nvec; }
+    size_t take;
+    if (!shared_gpu && left >= kBurstVecs32) { u = 32; take = kBurstVecs32; }
+    else if (!shared_gpu && left >= kBurstVecs16x3) { u = 16; take = kBurstVecs16x3; }
+    else if (left >= kBurstVecs16) { u = 16; take = kBurstVecs16; }
     else break;
-    const unsigned grid = (unsigned)((v1 - v0 + (size_t)kBurstBlock * u - 1) / ((size_t)kBurstBlock * u));
+    const size_t v1 = v0 + take;
+    const unsigned grid = (unsigned)(take / ((size_t)kBurstBlock * u));
     const Timing tq{v0 == 0 ? tm.start : nullptr, v1 == nvec ? tm.stop : nullptr};
     const unsigned eh = v0 == 0 ? head : 0, et = v0 == 0 ? tail : 0;
     switch (nsrc) {
@@ -678,7 +686,7 @@ hipError_t launch_burst(T* out, const SrcList<T>& sl, int nsrc, unsigned head, s
 
 template <typename T, int OP>
 hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipStream_t s, Timing tm,
-                          bool local_sources = true) {
+                          unsigned flags = 0) {
   SrcList<T> sl{};
   uintptr_t m = (uintptr_t)out & 15;
   bool congruent = (m % sizeof(T)) == 0;
@@ -691,9 +699,11 @@ hipError_t launch_multi_t(T* out, const T* const* srcs, int nsrc, size_t n, hipS
     size_t head = m ? (16 - m) / sizeof(T) : 0;
     if (head > n) head = n;
     size_t nvec = (n - head) / W, tail = (n - head) % W;
-    if (local_sources && g_fold_burst && nsrc >= 5 && nsrc <= 8 && nvec * 16 >= kBurstMinBytes) {
+    if (!(flags & PGK_FOLD_REMOTE_SOURCES) && g_fold_burst && nsrc >= 5 && nsrc <= 8 &&
+        nvec * 16 >= kBurstMinBytes) {
       size_t done = 0;
-      hipError_t e = launch_burst<T, OP>(out, sl, nsrc, (unsigned)head, nvec, (unsigned)tail, s, tm, &done);
+      hipError_t e = launch_burst<T, OP>(out, sl, nsrc, (unsigned)head, nvec, (unsigned)tail,
+                                         (flags & PGK_FOLD_SHARED_GPU) != 0, s, tm, &done);
       if (e != hipSuccess || done == nvec) return e;
       // the rest (under 32 MiB per source): one tile per wave, behind the bursts on the same stream
       out += head + done * W;
@@ -776,7 +786,11 @@ void launch_fold_bcast(void* const* outs, int nout, const unsigned char* area, s
 extern "C" {
 
 static int reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
-                        void* start_event, void* stop_event, bool local) {
+                        void* start_event, void* stop_event, unsigned flags) {
+  if (flags & ~(unsigned)(PGK_FOLD_REMOTE_SOURCES | PGK_FOLD_SHARED_GPU)) {
+    set_err("pgk: unknown fold flags 0x%x", flags);
+    return -1;
+  }
   if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
   if (op != PGK_OP_SUM && op != PGK_OP_PROD) { set_err("pgk: bad operation %d", op); return -1; }
   if (nsrc < 1 || nsrc > kMaxSrc) { set_err("pgk: nsrc %d outside 1..%d", nsrc, kMaxSrc); return -1; }
@@ -789,12 +803,12 @@ static int reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, 
   hipError_t e;
   if (dt == PGK_DT_INT32) {
     const uint32_t* const* x = (const uint32_t* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s, tm, local)
-                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s, tm, local);
+    e = op == PGK_OP_SUM ? launch_multi_t<uint32_t, PGK_OP_SUM>((uint32_t*)out, x, nsrc, n, s, tm, flags)
+                         : launch_multi_t<uint32_t, PGK_OP_PROD>((uint32_t*)out, x, nsrc, n, s, tm, flags);
   } else {
     const double* const* x = (const double* const*)srcs;
-    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s, tm, local)
-                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s, tm, local);
+    e = op == PGK_OP_SUM ? launch_multi_t<double, PGK_OP_SUM>((double*)out, x, nsrc, n, s, tm, flags)
+                         : launch_multi_t<double, PGK_OP_PROD>((double*)out, x, nsrc, n, s, tm, flags);
   }
   if (e != hipSuccess) { set_err("pgk: launch failed: %s", hipGetErrorString(e)); return -1; }
   return 0;
@@ -802,12 +816,12 @@ static int reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, 
 
 int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
                            void* start_event, void* stop_event) {
-  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, true);
+  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, 0);
 }
 
-int pgk_reduce_multi_remote_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op,
-                                  void* stream, void* start_event, void* stop_event) {
-  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, false);
+int pgk_fold_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, unsigned flags,
+                   void* stream, void* start_event, void* stop_event) {
+  return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, flags);
 }
 
 

@@ -20,6 +20,7 @@ REPO_ROOT = PKG_DIR.parent
 
 # include/pg.h (reference pg.h:78-87)
 DT_INT32, DT_DOUBLE = 0, 1
+FOLD_REMOTE_SOURCES, FOLD_SHARED_GPU = 1, 2        # pgk_fold_timed flags (include/pgk.h)
 OP_SUM, OP_PROD = 0, 1
 # include/pg_ext.h
 PG_TRANSPORT_RCCL, PG_TRANSPORT_LOOPBACK, PG_TRANSPORT_THREADS, PG_TRANSPORT_SELF, PG_TRANSPORT_XGMI = 0, 1, 2, 3, 4
@@ -115,7 +116,7 @@ _SIGS = {
     "pgk_reduce_ranges": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ),
                                _I, _I, _I, _VP, _VP, _VP]),
     "pgk_reduce_multi_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
-    "pgk_reduce_multi_remote_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
+    "pgk_fold_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, ctypes.c_uint, _VP, _VP, _VP]),
     "pgk_tune_fold": (_I, [_I]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),

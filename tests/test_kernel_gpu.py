@@ -334,8 +334,9 @@ def test_reduce_multi_burst_form(gpu, lib, oracle, nsrc, dt, op, nbytes, extra, 
     """From 5 sources and 32 MiB per source pgk_reduce_multi gathers its stores
     into one burst per launch (launches of at most 64 MiB per source).  Same
     left-to-right fold as nsrc-1 successive reduce_inplace steps (src/pg.c:151-159),
-    bit for bit; equal to the one-tile-per-wave form (pgk_tune_fold(0)) and to
-    the form for remote sources, byte for byte; stamped by its events."""
+    bit for bit; equal to the one-tile-per-wave form (pgk_tune_fold(0)), to
+    the form for remote sources and to the form for a shared GPU (32 MiB
+    launches), byte for byte; stamped by its events."""
     import ctypes
     torch = gpu
     es = 4 if dt == 0 else 8
@@ -359,7 +360,8 @@ def test_reduce_multi_burst_form(gpu, lib, oracle, nsrc, dt, op, nbytes, extra, 
         got = to_host(torch, out)
         assert got[shift:shift + n].tobytes() == want.tobytes()
         assert not got[:shift].any() and not got[shift + n:].any()           # nothing outside the range
-        for form in ("plain", "remote"):
+        for form in ("plain", pgamd.FOLD_REMOTE_SOURCES, pgamd.FOLD_SHARED_GPU,
+                     pgamd.FOLD_REMOTE_SOURCES | pgamd.FOLD_SHARED_GPU):
             other = torch.zeros(n + 4, dtype=D[0].dtype, device="cuda")
             if form == "plain":
                 assert lib.pgk_tune_fold(0) == 0
@@ -368,13 +370,17 @@ def test_reduce_multi_burst_form(gpu, lib, oracle, nsrc, dt, op, nbytes, extra, 
                 finally:
                     lib.pgk_tune_fold(1)
             else:
-                assert lib.pgk_reduce_multi_remote_timed(ptr(other) + shift * es, srcs, nsrc, n, dt, op, stream(torch),
-                                                         None, None) == 0
+                assert lib.pgk_fold_timed(ptr(other) + shift * es, srcs, nsrc, n, dt, op, form, stream(torch),
+                                          None, None) == 0
             assert torch.equal(other, out), form
             del other
+        assert lib.pgk_fold_timed(ptr(out), srcs, nsrc, n, dt, op, 4, stream(torch), None, None) == -1
+        assert b"unknown fold flags" in lib.pgk_last_error()
         lib.pgk_event_destroy(ev[0]), lib.pgk_event_destroy(ev[1])
     else:
-        assert lib.pgk_reduce_multi(ptr(D[inplace]) + shift * es, srcs, nsrc, n, dt, op, stream(torch)) == 0
+        flags = pgamd.FOLD_SHARED_GPU if nsrc == 5 else 0
+        assert lib.pgk_fold_timed(ptr(D[inplace]) + shift * es, srcs, nsrc, n, dt, op, flags, stream(torch),
+                                  None, None) == 0
         got = to_host(torch, D[inplace])
         assert got[shift:shift + n].tobytes() == want.tobytes()
         assert got[:shift].tobytes() == xs[inplace][:shift].tobytes()

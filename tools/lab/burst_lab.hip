@@ -69,6 +69,7 @@ static int pick(int unroll, int block, f64x2* o, Src8 s, size_t nvec, int blocks
     case 256 * 64 + 4: return go<R, 4, 256>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
     case 256 * 64 + 8: return go<R, 8, 256>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
     case 256 * 64 + 16: return go<R, 16, 256>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
+    case 256 * 64 + 24: return go<R, 24, 256>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
     case 256 * 64 + 32: return go<R, 32, 256>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
     case 512 * 64 + 8: return go<R, 8, 512>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
     case 512 * 64 + 16: return go<R, 16, 512>(o, s, nvec, blocks_per_cu, period, read_ticks, max_spins, st, a, b);
