@@ -451,6 +451,48 @@ def test_reduce_captured_in_hip_graph(gpu, lib, oracle):
         assert to_host(torch, A).tobytes() == want.tobytes(), (dt, op)
 
 
+def test_burst_fold_captured_in_hip_graph(gpu, lib, oracle):
+    """The fold's burst form is several plain kernel launches on the caller's
+    stream and allocates nothing: a 6-source fold of 72 MiB + 3 doubles per source
+    (one full launch, a rest one tile per wave, ragged edges), in place over its
+    last source, captured into a hipGraph.  Every replay, with eager work and a
+    synchronization between replays, equals the eager call on the same inputs."""
+    import ctypes
+    torch = gpu
+    nsrc, n = 6, (72 << 20) // 8 + 3
+    xs = [oracle.fill(n + 2, 1, 0, 7300 + j) for j in range(nsrc)]
+    D = [to_dev(torch, x) for x in xs]
+    srcs = (ctypes.c_void_p * nsrc)(*[ptr(d) + 8 for d in D])          # one element in: a ragged head
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            sh = torch.cuda.current_stream().cuda_stream
+            assert lib.pgk_reduce_multi(ptr(D[nsrc - 1]) + 8, srcs, nsrc, n, 1, 0, sh) == 0
+    for rep in range(3):
+        # fresh inputs for this replay (eager copies), the expected result by the eager call on copies of them
+        fresh = [oracle.fill(n + 2, 1, 0, 7400 + 10 * rep + j) for j in range(nsrc)]
+        for d, x in zip(D, fresh):
+            d.copy_(torch.from_numpy(x))
+        E = [d.clone() for d in D]
+        esrcs = (ctypes.c_void_p * nsrc)(*[ptr(e) + 8 for e in E])
+        assert lib.pgk_reduce_multi(ptr(E[nsrc - 1]) + 8, esrcs, nsrc, n, 1, 0, stream(torch)) == 0
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(D[nsrc - 1], E[nsrc - 1]), rep
+        want = fresh[0][1:1 + n].copy()
+        for j in range(1, nsrc):
+            want = oracle.reduce(want, fresh[j][1:1 + n], 1, 0)
+        got = to_host(torch, D[nsrc - 1])
+        assert got[1:1 + n].tobytes() == want.tobytes(), rep
+        assert got[0] == fresh[nsrc - 1][0] and got[1 + n] == fresh[nsrc - 1][1 + n]
+        del E
+    del D
+    torch.cuda.empty_cache()
+
+
 def test_reduce_ranges(gpu, lib, oracle):
     """pgk_reduce_ranges (one launch for every ring's arrived segments of an
     executor batch): 1..8 ranges of ragged lengths at aligned and misaligned
