@@ -225,8 +225,10 @@ __global__ __launch_bounds__(kMultiVecBlock) void k_reduce_multi_vec(T* __restri
 //       beside 128 resident workgroups of 256 lanes x 128 VGPRs; it also fits
 //       beside waves of 256 VGPRs, which RCCL's kernels are
 // (tools/lab/burst_occupied_probe2.py).  So a fold that has the GPU to itself
-// is cut into 64 MiB launches, and one that runs beside communication kernels
-// (PGK_FOLD_SHARED_GPU) into 32 MiB ones.  It does not pay below five sources
+// is cut into 64 MiB launches and a last one of 32 .. 64 MiB at 16 tiles per
+// wave (up to four workgroups per CU; between whole numbers per CU it runs at
+// 76-78%, still above one tile per wave), and one that runs beside
+// communication kernels (PGK_FOLD_SHARED_GPU) into 32 MiB ones.  It does not pay below five sources
 // or 32 MiB per source.
 // A lane reads its elements of every source before it writes them, so out may
 // be one of the sources, as in the kernel above.
@@ -234,7 +236,6 @@ constexpr int kBurstBlock = 256;
 constexpr int kBurstBlocks = 512;                  // workgroups per launch: two per CU
 constexpr size_t kBurstMinBytes = 32u << 20;       // per source, whole call
 constexpr size_t kBurstVecs32 = (size_t)kBurstBlocks * kBurstBlock * 32;       // 64 MiB per source
-constexpr size_t kBurstVecs16x3 = (size_t)kBurstBlocks / 2 * 3 * kBurstBlock * 16;   // 48 MiB, three per CU
 constexpr size_t kBurstVecs16 = (size_t)kBurstBlocks * kBurstBlock * 16;       // 32 MiB
 
 template <typename T, int OP, int NS, int U>
@@ -663,11 +664,11 @@ hipError_t launch_burst(T* out, const SrcList<T>& sl, int nsrc, unsigned head, s
     int u;
     size_t take;
     if (!shared_gpu && left >= kBurstVecs32) { u = 32; take = kBurstVecs32; }
-    else if (!shared_gpu && left >= kBurstVecs16x3) { u = 16; take = kBurstVecs16x3; }
+    else if (!shared_gpu && left >= kBurstVecs16) { u = 16; take = left; }        /* 512 .. 1023 workgroups */
     else if (left >= kBurstVecs16) { u = 16; take = kBurstVecs16; }
     else break;
     const size_t v1 = v0 + take;
-    const unsigned grid = (unsigned)(take / ((size_t)kBurstBlock * u));
+    const unsigned grid = (unsigned)((take + (size_t)kBurstBlock * u - 1) / ((size_t)kBurstBlock * u));
     const Timing tq{v0 == 0 ? tm.start : nullptr, v1 == nvec ? tm.stop : nullptr};
     const unsigned eh = v0 == 0 ? head : 0, et = v0 == 0 ? tail : 0;
     switch (nsrc) {
