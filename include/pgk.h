@@ -93,6 +93,15 @@ PG_API int pgk_reduce_multi_timed(void *out, const void *const *srcs, int nsrc, 
 PG_API int pgk_fold_timed(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op, unsigned flags,
                           void *stream, void *start_event, void *stop_event);
 
+/* How pgk_fold_timed would cut a fold of n elements per source (operands
+ * 16-byte aligned) with these flags: returns the number of burst launches and
+ * fills the first max_launches entries of launch_bytes (bytes per source) and
+ * launch_tiles (tiles per wave); *plain_bytes = what is folded one tile per
+ * wave (everything, when the burst form does not apply).  Host arithmetic
+ * only: for tests and benches. */
+PG_API int pgk_fold_geometry(size_t n, int dt, int nsrc, unsigned flags, size_t *launch_bytes, int *launch_tiles,
+                             int max_launches, size_t *plain_bytes);
+
 /* One-shot all-reduce fold: element i lies in ring block b = i / block_elems
  * and out[i] = srcs[(b+1)%k][i] op srcs[(b+2)%k][i] op ... op srcs[b][i]
  * (k = nsrc; requires ceil(n / block_elems) <= k): block b folded in exactly

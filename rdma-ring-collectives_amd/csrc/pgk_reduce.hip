@@ -650,6 +650,16 @@ void launch_burst_u(int u, unsigned grid, T* out, const SrcList<T>& sl, unsigned
 #undef PGK_BURST_CASE
 }
 
+// The next burst launch of a call with `left` vectors per source still to fold:
+// how many vectors it takes and with how many tiles per wave; 0 = none (what
+// is left goes one tile per wave).
+inline size_t burst_next(size_t left, bool shared_gpu, int* tiles) {
+  if (!shared_gpu && left >= kBurstVecs32) { *tiles = 32; return kBurstVecs32; }
+  if (!shared_gpu && left >= kBurstVecs16) { *tiles = 16; return left; }          // 512 .. 1023 workgroups
+  if (left >= kBurstVecs16) { *tiles = 16; return kBurstVecs16; }
+  return 0;
+}
+
 // The burst fold of a whole call (5 <= nsrc <= 8, nvec * 16 >= kBurstMinBytes),
 // as whole launches of the shapes above; what is left (under 32 MiB per source)
 // is returned to the caller (`done` = vectors covered), which folds it one tile
@@ -660,13 +670,9 @@ hipError_t launch_burst(T* out, const SrcList<T>& sl, int nsrc, unsigned head, s
   const size_t tail_e = head + nvec * (16 / sizeof(T));
   size_t v0 = 0;
   while (v0 < nvec) {
-    const size_t left = nvec - v0;
     int u;
-    size_t take;
-    if (!shared_gpu && left >= kBurstVecs32) { u = 32; take = kBurstVecs32; }
-    else if (!shared_gpu && left >= kBurstVecs16) { u = 16; take = left; }        /* 512 .. 1023 workgroups */
-    else if (left >= kBurstVecs16) { u = 16; take = kBurstVecs16; }
-    else break;
+    const size_t take = burst_next(nvec - v0, shared_gpu, &u);
+    if (!take) break;
     const size_t v1 = v0 + take;
     const unsigned grid = (unsigned)((take + (size_t)kBurstBlock * u - 1) / ((size_t)kBurstBlock * u));
     const Timing tq{v0 == 0 ? tm.start : nullptr, v1 == nvec ? tm.stop : nullptr};
@@ -818,6 +824,30 @@ static int reduce_multi(void* out, const void* const* srcs, int nsrc, size_t n, 
 int pgk_reduce_multi_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, void* stream,
                            void* start_event, void* stop_event) {
   return reduce_multi(out, srcs, nsrc, n, dt, op, stream, start_event, stop_event, 0);
+}
+
+int pgk_fold_geometry(size_t n, int dt, int nsrc, unsigned flags, size_t* launch_bytes, int* launch_tiles,
+                      int max_launches, size_t* plain_bytes) {
+  if (dt != PGK_DT_INT32 && dt != PGK_DT_DOUBLE) { set_err("pgk: bad datatype %d", dt); return -1; }
+  if (nsrc < 1 || nsrc > kMaxSrc || max_launches < 0 || (max_launches && (!launch_bytes || !launch_tiles))) {
+    set_err("pgk: bad fold geometry arguments");
+    return -1;
+  }
+  const size_t es = dt == PGK_DT_INT32 ? 4 : 8;
+  size_t left = n * es / 16;                      // 16-byte-aligned operands: no edge elements
+  int k = 0;
+  if (!(flags & PGK_FOLD_REMOTE_SOURCES) && g_fold_burst && nsrc >= 5 && nsrc <= 8 && left * 16 >= kBurstMinBytes) {
+    for (;;) {
+      int tiles = 0;
+      const size_t take = burst_next(left, (flags & PGK_FOLD_SHARED_GPU) != 0, &tiles);
+      if (!take) break;
+      if (k < max_launches) { launch_bytes[k] = take * 16; launch_tiles[k] = tiles; }
+      ++k;
+      left -= take;
+    }
+  }
+  if (plain_bytes) *plain_bytes = left * 16 + n * es % 16;
+  return k;
 }
 
 int pgk_fold_timed(void* out, const void* const* srcs, int nsrc, size_t n, int dt, int op, unsigned flags,

@@ -118,6 +118,8 @@ _SIGS = {
     "pgk_reduce_multi_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP, _VP, _VP]),
     "pgk_fold_timed": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, ctypes.c_uint, _VP, _VP, _VP]),
     "pgk_tune_fold": (_I, [_I]),
+    "pgk_fold_geometry": (_I, [_SZ, _I, _I, ctypes.c_uint, ctypes.POINTER(_SZ), ctypes.POINTER(_I), _I,
+                               ctypes.POINTER(_SZ)]),
     "pgk_reduce_multi": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _I, _I, _VP]),
     "pgk_fold_blocks": (_I, [_VP, ctypes.POINTER(_VP), _I, _SZ, _SZ, _I, _I, _I, _VP]),
     "pgk_gather": (_I, [ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_SZ), _I, _VP]),

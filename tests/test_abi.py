@@ -98,3 +98,45 @@ def test_headers_compile_as_c_and_cpp(tmp_path):
     subprocess.run(["make", "-s", "-C", str(pgamd.PKG_DIR), "install", f"DESTDIR={tmp_path}", "PREFIX=/opt/pg"],
                    check=True)
     assert (tmp_path / "opt/pg/lib/libpg_amd.so").exists() and (tmp_path / "opt/pg/include/pg.h").exists()
+
+
+def test_fold_launch_rule(lib):
+    """How pgk_reduce_multi / pgk_fold_timed cut a fold into launches (host
+    arithmetic, no device): the burst form from 5 to 8 sources and 32 MiB per
+    source; 64 MiB launches of 32 tiles per wave and a last one of 32-64 MiB at
+    16 tiles when the fold has the GPU to itself, 32 MiB launches beside other
+    kernels, never for remote sources; the rest one tile per wave."""
+    MiB = 1 << 20
+    SZ, I = ctypes.c_size_t, ctypes.c_int
+
+    def cut(nbytes, nsrc=8, flags=0, dt=pgamd.DT_DOUBLE):
+        es = 8 if dt == pgamd.DT_DOUBLE else 4
+        lb, lt, plain = (SZ * 8)(), (I * 8)(), SZ()
+        k = lib.pgk_fold_geometry(nbytes // es, dt, nsrc, flags, lb, lt, 8, ctypes.byref(plain))
+        assert k >= 0, pgamd.last_error()
+        return [(lb[i] // MiB, lt[i]) for i in range(min(k, 8))], plain.value / MiB, k
+
+    assert cut(64 * MiB) == ([(64, 32)], 0, 1)
+    assert cut(64 * MiB, dt=pgamd.DT_INT32) == ([(64, 32)], 0, 1)
+    assert cut(256 * MiB) == ([(64, 32)] * 4, 0, 4)
+    assert cut(72 * MiB) == ([(64, 32)], 8, 1)                      # a rest under 32 MiB: one tile per wave
+    assert cut(100 * MiB) == ([(64, 32), (36, 16)], 0, 2)           # a rest of 32-64 MiB: one 16-tile launch
+    assert cut(40 * MiB) == ([(40, 16)], 0, 1)
+    assert cut(32 * MiB) == ([(32, 16)], 0, 1)
+    assert cut(31 * MiB) == ([], 31, 0)                             # under 32 MiB per source: plain
+    assert cut(64 * MiB, nsrc=4) == ([], 64, 0) and cut(64 * MiB, nsrc=9) == ([], 64, 0)
+    assert cut(64 * MiB, nsrc=5)[0] == [(64, 32)]
+    shared = pgamd.FOLD_SHARED_GPU
+    assert cut(64 * MiB, flags=shared) == ([(32, 16), (32, 16)], 0, 2)
+    assert cut(100 * MiB, flags=shared) == ([(32, 16)] * 3, 4, 3)
+    assert cut(256 * MiB, flags=pgamd.FOLD_REMOTE_SOURCES) == ([], 256, 0)
+    assert cut(256 * MiB, flags=pgamd.FOLD_REMOTE_SOURCES | shared) == ([], 256, 0)
+    # the API's largest double count: 256 launches, the first 8 reported
+    first, plain, k = cut(((1 << 31) - 1) * 8)
+    assert k == 256 and first == [(64, 32)] * 8 and plain < 1 / 1024 * 64
+    assert lib.pgk_tune_fold(0) == 0
+    try:
+        assert cut(256 * MiB) == ([], 256, 0)
+    finally:
+        lib.pgk_tune_fold(1)
+    assert lib.pgk_fold_geometry(8, 2, 8, 0, None, None, 0, None) == -1
