@@ -64,8 +64,9 @@ PG_API int pgk_reduce_ranges(void *const *outs, const void *const *as, const voi
 
 /* out[i] = ((srcs[0][i] op srcs[1][i]) op srcs[2][i]) ... op srcs[nsrc-1][i],
  * folded left to right (1 <= nsrc <= 16).  Sources may be peer GPUs' memory
- * mapped through HIP IPC (read over xGMI).  With srcs in ring order this is
- * bit-identical to the W-1 ring steps of reduce_inplace it fuses. */
+ * mapped through HIP IPC (read over xGMI; a caller whose sources are mostly
+ * remote says so through pgk_fold_timed below).  With srcs in ring order this
+ * is bit-identical to the W-1 ring steps of reduce_inplace it fuses. */
 PG_API int pgk_reduce_multi(void *out, const void *const *srcs, int nsrc, size_t n, int dt, int op,
                      void *stream);
 /* The same launch with the kernel's own begin/end timestamps recorded into two
