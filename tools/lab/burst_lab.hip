@@ -108,3 +108,68 @@ extern "C" int burst_launch(int unroll, int block, int blocks_per_cu, unsigned p
                             void* e1) {
   return burst_launch_k(8, unroll, block, blocks_per_cu, period, read_ticks, max_spins, out, srcs, n, stream, e0, e1);
 }
+
+// The same kernel (8 sources, 256 lanes) with its burst of stores issued as
+// buffer stores carrying the cache-policy bits AUX (gfx950: sc0 = 1, nt = 2,
+// sc1 = 16; 0 = plain): does the policy of a DENSE run of stores matter?
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void k_burst_pol(f64x2* __restrict__ out, Src8 s, size_t nvec) {
+  constexpr int B = 256;
+  const size_t tile0 = (size_t)blockIdx.x * B * U;
+  if (tile0 >= nvec) return;
+  f64x2 r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t i = tile0 + (size_t)u * B + threadIdx.x;
+    if (i < nvec) {
+      f64x2 x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = __builtin_nontemporal_load(s.p[j] + i);
+      f64x2 acc = x[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) acc += x[j];
+      r[u] = acc;
+    }
+  }
+  asm volatile("" ::: "memory");
+  const size_t left = nvec - tile0;
+  const uint32_t bytes = (uint32_t)((left < (size_t)B * U ? left : (size_t)B * U) * sizeof(f64x2));
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + tile0, (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t i = tile0 + (size_t)u * B + threadIdx.x;
+    if (i < nvec)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, r[u]), rs,
+                                             (int)((threadIdx.x + u * B) * sizeof(f64x2)), 0, AUX);
+  }
+}
+
+template <int U, int AUX>
+static int go_pol(f64x2* o, Src8 s, size_t nvec, hipStream_t st, hipEvent_t a, hipEvent_t b) {
+  const unsigned grid = (unsigned)((nvec + 256 * (size_t)U - 1) / (256 * (size_t)U));
+  hipExtLaunchKernelGGL((k_burst_pol<U, AUX>), dim3(grid), dim3(256), 0, st, a, b, 0, o, s, nvec);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int burst_policy_launch(int unroll, int aux, double* out, const double* const* srcs, size_t n, void* stream,
+                                   void* e0, void* e1) {
+  if (n & 1) return -1;
+  Src8 s;
+  for (int j = 0; j < 8; ++j) s.p[j] = (const f64x2*)srcs[j];
+  hipStream_t st = (hipStream_t)stream;
+  hipEvent_t a = (hipEvent_t)e0, b = (hipEvent_t)e1;
+  f64x2* o = (f64x2*)out;
+  const size_t nvec = n / 2;
+  switch (unroll * 100 + aux) {
+    case 3200: return go_pol<32, 0>(o, s, nvec, st, a, b);
+    case 3202: return go_pol<32, 2>(o, s, nvec, st, a, b);
+    case 3216: return go_pol<32, 16>(o, s, nvec, st, a, b);
+    case 3218: return go_pol<32, 18>(o, s, nvec, st, a, b);
+    case 3201: return go_pol<32, 1>(o, s, nvec, st, a, b);
+    case 1600: return go_pol<16, 0>(o, s, nvec, st, a, b);
+    case 1602: return go_pol<16, 2>(o, s, nvec, st, a, b);
+    case 1616: return go_pol<16, 16>(o, s, nvec, st, a, b);
+    default: return -1;
+  }
+}
